@@ -1,0 +1,140 @@
+"""Control model surface (reference ``control.py``): standard causal softmax
+attention with RoPE.  It is the comparison baseline, not the hot path (SURVEY
+section 2, C5), and is carried as PyTorch: the per-head projections are packed
+into one GEMM and the causal attention runs through
+``torch.nn.functional.scaled_dot_product_attention`` (no T x T ``tril`` or
+materialised map).  Routing it through the N=1 fused kernel is a section 8(f)
+"next" item.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+from torch.nn import functional as F
+
+from ._compat import emit_tril_hooks, check_seq_len
+from .Ndiff_transformer import precompute_freqs_cis, apply_rotary_emb
+
+__all__ = ["precompute_freqs_cis", "apply_rotary_emb", "Head", "MultiHeadAttention", "SwiGLU", "Block",
+           "StandardTransformer"]
+
+
+def _rope_fp32(x: torch.Tensor, freqs_cis: torch.Tensor) -> torch.Tensor:
+    # x (B, H, T, hs); interleaved pairs rotated in fp32 then cast back (control.py:11-22)
+    T = x.shape[2]
+    xc = torch.view_as_complex(x.float().reshape(*x.shape[:-1], -1, 2))
+    return torch.view_as_real(xc * freqs_cis[:T].to(x.device)).flatten(-2).type_as(x)
+
+
+class Head(nn.Module):
+    """One RoPE causal head (control.py:24-63)."""
+
+    def __init__(self, head_size, n_embd, dropout, block_size):
+        super().__init__()
+        self.key = nn.Linear(n_embd, head_size, bias=False)
+        self.query = nn.Linear(n_embd, head_size, bias=False)
+        self.value = nn.Linear(n_embd, head_size, bias=False)
+        self.block_size = block_size
+        self.head_size = head_size
+        emit_tril_hooks(self, block_size)
+        self.dropout = nn.Dropout(dropout)
+        self.register_buffer("freqs_cis", precompute_freqs_cis(head_size, block_size))
+
+    def forward(self, x):
+        check_seq_len(x.shape[1], self.block_size)
+        q = _rope_fp32(self.query(x)[:, None], self.freqs_cis)
+        k = _rope_fp32(self.key(x)[:, None], self.freqs_cis)
+        v = self.value(x)[:, None]
+        p = self.dropout.p if self.training else 0.0
+        out = F.scaled_dot_product_attention(q, k, v, is_causal=True, dropout_p=p,
+                                             scale=1.0 / (self.head_size ** 0.5))
+        return out[:, 0]
+
+
+class MultiHeadAttention(nn.Module):
+    """control.py:64-78 with the H per-head projections packed into one GEMM."""
+
+    def __init__(self, num_heads, head_size, n_embd, dropout, block_size):
+        super().__init__()
+        self.heads = nn.ModuleList([Head(head_size, n_embd, dropout, block_size) for _ in range(num_heads)])
+        self.proj = nn.Linear(head_size * num_heads, n_embd)
+        self.dropout = nn.Dropout(dropout)
+        self.num_heads = num_heads
+        self.head_size = head_size
+
+    def forward(self, x):
+        B, T, _ = x.shape
+        check_seq_len(T, self.heads[0].block_size)
+        H, hs = self.num_heads, self.head_size
+        w = torch.cat([h.query.weight for h in self.heads] + [h.key.weight for h in self.heads]
+                      + [h.value.weight for h in self.heads], 0)
+        q, k, v = F.linear(x, w).view(B, T, 3, H, hs).permute(2, 0, 3, 1, 4)
+        fc = self.heads[0].freqs_cis
+        q, k = _rope_fp32(q, fc), _rope_fp32(k, fc)
+        p = self.heads[0].dropout.p if self.training else 0.0
+        out = F.scaled_dot_product_attention(q, k, v, is_causal=True, dropout_p=p, scale=1.0 / (hs ** 0.5))
+        out = out.transpose(1, 2).reshape(B, T, H * hs)
+        return self.dropout(self.proj(out))
+
+
+class SwiGLU(nn.Module):
+    def __init__(self, size_in, size_out):
+        super().__init__()
+        self.linear_gate = nn.Linear(size_in, size_out)
+        self.linear_xform = nn.Linear(size_in, size_out)
+
+    def forward(self, x):
+        return F.silu(self.linear_gate(x)) * self.linear_xform(x)
+
+
+class Block(nn.Module):
+    """control.py:92-111 (head_size = n_embd // n_head)."""
+
+    def __init__(self, n_embd, n_head, block_size, dropout):
+        super().__init__()
+        self.attn = MultiHeadAttention(n_head, n_embd // n_head, n_embd, dropout, block_size)
+        self.ffwd = nn.Sequential(SwiGLU(n_embd, 4 * n_embd), nn.Linear(4 * n_embd, n_embd), nn.Dropout(dropout))
+        self.ln1 = nn.LayerNorm(n_embd)
+        self.ln2 = nn.LayerNorm(n_embd)
+
+    def forward(self, x):
+        x = x + self.attn(self.ln1(x))
+        return x + self.ffwd(self.ln2(x))
+
+
+class StandardTransformer(nn.Module):
+    """control.py:113-171."""
+
+    def __init__(self, vocab_size, n_embd, n_head, n_layer, block_size, dropout):
+        super().__init__()
+        self.block_size = block_size
+        self.token_embedding_table = nn.Embedding(vocab_size, n_embd)
+        self.blocks = nn.ModuleList([Block(n_embd, n_head, block_size, dropout) for _ in range(n_layer)])
+        self.ln_f = nn.LayerNorm(n_embd)
+        self.lm_head = nn.Linear(n_embd, vocab_size)
+        self.apply(self._init_weights)
+
+    def _init_weights(self, module):
+        if isinstance(module, (nn.Linear, nn.Embedding)):
+            nn.init.normal_(module.weight, mean=0.0, std=0.02)
+            if isinstance(module, nn.Linear) and module.bias is not None:
+                nn.init.zeros_(module.bias)
+
+    def forward(self, idx, targets=None):
+        B, T = idx.shape
+        x = self.token_embedding_table(idx)
+        for block in self.blocks:
+            x = block(x)
+        logits = self.lm_head(self.ln_f(x))
+        loss = None
+        if targets is not None:
+            loss = F.cross_entropy(logits.view(B * T, -1), targets.view(B * T))
+        return logits, loss
+
+    @torch.no_grad()
+    def generate(self, idx, max_new_tokens):
+        for _ in range(max_new_tokens):
+            logits, _ = self(idx[:, -self.block_size:])
+            probs = F.softmax(logits[:, -1, :], dim=-1)
+            idx = torch.cat((idx, torch.multinomial(probs, num_samples=1)), dim=1)
+        return idx

@@ -1,0 +1,8 @@
+// attn_bf16.hip -- __bf16 instantiations of the attention kernels (attn_kernels.h).
+#include "attn_kernels.h"
+
+namespace dta {
+int launch_attn_fwd_bf16(const FwdParams& p, hipStream_t st) { return dispatch_fwd<__bf16>(p, st); }
+int launch_attn_bwd_bf16(const BwdParams& p, hipStream_t st) { return dispatch_bwd<__bf16>(p, st); }
+bool attn_supported_bf16(int hs, int n) { return supported_t<__bf16>(hs, n); }
+}  // namespace dta

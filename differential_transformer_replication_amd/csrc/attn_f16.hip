@@ -1,0 +1,8 @@
+// attn_f16.hip -- _Float16 instantiations of the attention kernels (attn_kernels.h).
+#include "attn_kernels.h"
+
+namespace dta {
+int launch_attn_fwd_f16(const FwdParams& p, hipStream_t st) { return dispatch_fwd<_Float16>(p, st); }
+int launch_attn_bwd_f16(const BwdParams& p, hipStream_t st) { return dispatch_bwd<_Float16>(p, st); }
+bool attn_supported_f16(int hs, int n) { return supported_t<_Float16>(hs, n); }
+}  // namespace dta

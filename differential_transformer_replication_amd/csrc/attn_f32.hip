@@ -1,0 +1,8 @@
+// attn_f32.hip -- float instantiations of the attention kernels (attn_kernels.h).
+#include "attn_kernels.h"
+
+namespace dta {
+int launch_attn_fwd_f32(const FwdParams& p, hipStream_t st) { return dispatch_fwd<float>(p, st); }
+int launch_attn_bwd_f32(const BwdParams& p, hipStream_t st) { return dispatch_bwd<float>(p, st); }
+bool attn_supported_f32(int hs, int n) { return supported_t<float>(hs, n); }
+}  // namespace dta

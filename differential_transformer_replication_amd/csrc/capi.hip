@@ -1,0 +1,211 @@
+// capi.hip -- the extern "C" boundary of libdiffattn.so (include/diffattn.h).
+// Validates every argument, then enqueues kernels on the caller's stream.
+// Nothing here allocates, synchronises or keeps state.
+#include "../../include/diffattn.h"
+#include "dta_internal.h"
+
+namespace dta {
+int launch_attn_fwd_bf16(const FwdParams&, hipStream_t);
+int launch_attn_fwd_f16(const FwdParams&, hipStream_t);
+int launch_attn_fwd_f32(const FwdParams&, hipStream_t);
+int launch_attn_bwd_bf16(const BwdParams&, hipStream_t);
+int launch_attn_bwd_f16(const BwdParams&, hipStream_t);
+int launch_attn_bwd_f32(const BwdParams&, hipStream_t);
+bool attn_supported_bf16(int, int);
+bool attn_supported_f16(int, int);
+bool attn_supported_f32(int, int);
+
+int launch_attn_fwd(int dtype, const FwdParams& p, hipStream_t st) {
+  switch (dtype) {
+    case DTA_BF16: return launch_attn_fwd_bf16(p, st);
+    case DTA_F16: return launch_attn_fwd_f16(p, st);
+    case DTA_F32: return launch_attn_fwd_f32(p, st);
+  }
+  return -2;
+}
+int launch_attn_bwd(int dtype, const BwdParams& p, hipStream_t st) {
+  switch (dtype) {
+    case DTA_BF16: return launch_attn_bwd_bf16(p, st);
+    case DTA_F16: return launch_attn_bwd_f16(p, st);
+    case DTA_F32: return launch_attn_bwd_f32(p, st);
+  }
+  return -2;
+}
+bool attn_supported(int dtype, int hs, int n, int dv) {
+  if (dv != 2 * hs) return false;
+  switch (dtype) {
+    case DTA_BF16: return attn_supported_bf16(hs, n);
+    case DTA_F16: return attn_supported_f16(hs, n);
+    case DTA_F32: return attn_supported_f32(hs, n);
+  }
+  return false;
+}
+}  // namespace dta
+
+using namespace dta;
+
+namespace {
+
+constexpr float kLog2e = 1.4426950408889634f;
+
+int esize(int dtype) { return dtype == DTA_F32 ? 4 : 2; }
+
+// element alignment every pointer/stride must have: one 16-byte vector
+int vec_elems(int dtype) { return 16 / esize(dtype); }
+
+bool aligned_ptr(const void* p) { return p && (reinterpret_cast<uintptr_t>(p) % 16) == 0; }
+
+bool ok_tensor(const dta_tensor& t, int dtype, bool with_i) {
+  const int64_t v = vec_elems(dtype);
+  if (!aligned_ptr(t.ptr)) return false;
+  if (t.sb % v || t.st % v || t.sh % v) return false;
+  if (with_i && t.si % v) return false;
+  return t.sb >= 0 && t.st >= 0 && t.sh >= 0 && t.si >= 0;
+}
+
+T5 t5(const dta_tensor& t) { return T5{t.ptr, t.sb, t.st, t.sh, t.si}; }
+
+int status(int e) {
+  if (e == 0) return DTA_OK;
+  if (e == -2) return DTA_ERR_UNSUPPORTED;
+  return DTA_ERR_LAUNCH;
+}
+
+bool ok_dims(int dtype, int B, int T, int H, int N, int hs, int dv) {
+  if (dtype < DTA_BF16 || dtype > DTA_F32) return false;
+  return B >= 0 && T >= 0 && H > 0 && N > 0 && hs > 0 && dv > 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dta_abi_version(void) { return DTA_ABI_VERSION; }
+
+const char* dta_error_string(int code) {
+  switch (code) {
+    case DTA_OK: return "ok";
+    case DTA_ERR_INVALID: return "invalid argument (shape, null/misaligned pointer or stride)";
+    case DTA_ERR_UNSUPPORTED: return "unsupported configuration (head_size/n_terms/dtype not built for gfx950)";
+    case DTA_ERR_LAUNCH: return "HIP launch failed";
+    case DTA_ERR_DROPOUT: return "attention dropout p > 0 is not supported by the fused kernels";
+  }
+  return "unknown error";
+}
+
+int dta_supported(int32_t dtype, int32_t head_size, int32_t n_terms, int32_t dv) {
+  return attn_supported(dtype, head_size, n_terms, dv) ? 1 : 0;
+}
+
+int dta_attn_fwd(const dta_attn_fwd_args* a, void* stream) {
+  if (!a) return DTA_ERR_INVALID;
+  if (!ok_dims(a->dtype, a->B, a->T, a->H, a->n_terms, a->head_size, a->dv)) return DTA_ERR_INVALID;
+  if (a->dropout_p != 0.f) return DTA_ERR_DROPOUT;
+  if (!attn_supported(a->dtype, a->head_size, a->n_terms, a->dv)) return DTA_ERR_UNSUPPORTED;
+  if ((int64_t)a->B * a->T == 0) return DTA_OK;
+  if (!ok_tensor(a->q, a->dtype, true) || !ok_tensor(a->k, a->dtype, true) || !ok_tensor(a->v, a->dtype, false) ||
+      !ok_tensor(a->o, a->dtype, false) || !ok_tensor(a->obr, a->dtype, true) || !a->lse || !a->coef)
+    return DTA_ERR_INVALID;
+  FwdParams p{};
+  p.q = t5(a->q); p.k = t5(a->k); p.v = t5(a->v); p.o = t5(a->o); p.obr = t5(a->obr);
+  p.lse = a->lse; p.coef = a->coef;
+  p.B = a->B; p.T = a->T; p.H = a->H; p.N = a->n_terms; p.HS = a->head_size; p.DV = a->dv;
+  p.sl2 = a->scale * kLog2e;
+  return status(launch_attn_fwd(a->dtype, p, (hipStream_t)stream));
+}
+
+size_t dta_attn_bwd_workspace_bytes(int32_t B, int32_t T, int32_t H, int32_t n_terms, int32_t head_size) {
+  const size_t delta = (size_t)n_terms * B * H * T * 4;
+  const size_t dq = (size_t)B * T * H * n_terms * head_size * 4;
+  return delta + dq;
+}
+
+int dta_attn_bwd(const dta_attn_bwd_args* a, void* stream) {
+  if (!a) return DTA_ERR_INVALID;
+  if (!ok_dims(a->dtype, a->B, a->T, a->H, a->n_terms, a->head_size, a->dv)) return DTA_ERR_INVALID;
+  if (a->dropout_p != 0.f) return DTA_ERR_DROPOUT;
+  if (!attn_supported(a->dtype, a->head_size, a->n_terms, a->dv)) return DTA_ERR_UNSUPPORTED;
+  if (!a->dcoef) return DTA_ERR_INVALID;
+  hipStream_t st = (hipStream_t)stream;
+  if ((int64_t)a->B * a->T == 0) {
+    return status((int)hipMemsetAsync(a->dcoef, 0, sizeof(float) * a->H * a->n_terms, st));
+  }
+  if (!ok_tensor(a->q, a->dtype, true) || !ok_tensor(a->k, a->dtype, true) || !ok_tensor(a->v, a->dtype, false) ||
+      !ok_tensor(a->obr, a->dtype, true) || !ok_tensor(a->dout, a->dtype, false) ||
+      !ok_tensor(a->dk, a->dtype, true) || !ok_tensor(a->dv_out, a->dtype, false) ||
+      !a->lse || !a->coef || !a->delta || !aligned_ptr(a->dq_f32))
+    return DTA_ERR_INVALID;
+  if (a->dq.ptr && !ok_tensor(a->dq, a->dtype, true)) return DTA_ERR_INVALID;
+  const int B = a->B, T = a->T, H = a->H, N = a->n_terms, HS = a->head_size;
+  int e = (int)hipMemsetAsync(a->dq_f32, 0, (size_t)B * T * H * N * HS * 4, st);
+  if (e) return DTA_ERR_LAUNCH;
+  DeltaParams dp{};
+  dp.dout = t5(a->dout); dp.obr = t5(a->obr); dp.delta = a->delta;
+  dp.B = B; dp.T = T; dp.H = H; dp.N = N; dp.DV = a->dv;
+  if ((e = launch_delta(a->dtype, dp, st))) return status(e);
+  if ((e = launch_dcoef(a->delta, a->dcoef, B, T, H, N, st))) return status(e);
+  BwdParams p{};
+  p.q = t5(a->q); p.k = t5(a->k); p.v = t5(a->v); p.dout = t5(a->dout);
+  p.dk = t5(a->dk); p.dv = t5(a->dv_out);
+  p.lse = a->lse; p.delta = a->delta; p.coef = a->coef; p.dq = a->dq_f32;
+  p.B = B; p.T = T; p.H = H; p.N = N; p.HS = HS; p.DV = a->dv;
+  p.scale = a->scale; p.sl2 = a->scale * kLog2e;
+  if ((e = launch_attn_bwd(a->dtype, p, st))) return status(e);
+  if (a->dq.ptr) {
+    if ((e = launch_cast(a->dtype, a->dq_f32, t5(a->dq), B, T, H, N, HS, st))) return status(e);
+  }
+  return DTA_OK;
+}
+
+static int ln_common(const dta_ln_args* a, bool bwd) {
+  if (!a || a->dtype < DTA_BF16 || a->dtype > DTA_F32 || a->rows < 0 || a->C <= 0) return DTA_ERR_INVALID;
+  const int64_t v = 8;   // kernels move 8 elements per lane access
+  if (a->C % v || a->C > 8192) return DTA_ERR_UNSUPPORTED;
+  if (!aligned_ptr(a->x) || a->x_stride % v || !a->w || !a->mean || !a->rstd) return DTA_ERR_INVALID;
+  if (!bwd && (!aligned_ptr(a->y) || a->y_stride % v || !a->b)) return DTA_ERR_INVALID;
+  if (bwd && (!aligned_ptr(a->dy) || !aligned_ptr(a->dx) || a->dy_stride % v || a->dx_stride % v || !a->dw || !a->db))
+    return DTA_ERR_INVALID;
+  return DTA_OK;
+}
+
+static LnParams ln_params(const dta_ln_args* a) {
+  LnParams p{};
+  p.rows = a->rows; p.C = a->C; p.eps = a->eps; p.out_scale = a->out_scale;
+  p.x = a->x; p.xs = a->x_stride; p.y = a->y; p.ys = a->y_stride;
+  p.w = a->w; p.b = a->b; p.mean = a->mean; p.rstd = a->rstd;
+  p.dy = a->dy; p.dys = a->dy_stride; p.dx = a->dx; p.dxs = a->dx_stride;
+  p.dw = a->dw; p.db = a->db;
+  return p;
+}
+
+int dta_ln_fwd(const dta_ln_args* a, void* stream) {
+  if (int e = ln_common(a, false)) return e;
+  return status(launch_ln(a->dtype, ln_params(a), false, (hipStream_t)stream));
+}
+
+int dta_ln_bwd(const dta_ln_args* a, void* stream) {
+  if (int e = ln_common(a, true)) return e;
+  return status(launch_ln(a->dtype, ln_params(a), true, (hipStream_t)stream));
+}
+
+int dta_rope(const dta_rope_args* a, void* stream) {
+  if (!a || !ok_dims(a->dtype, a->B, a->T, a->H, a->n_terms, a->head_size, 1)) return DTA_ERR_INVALID;
+  if (a->head_size % 8) return DTA_ERR_UNSUPPORTED;
+  if ((int64_t)a->B * a->T == 0) return DTA_OK;
+  const int src_dtype = a->src_f32 ? DTA_F32 : a->dtype;
+  if (!ok_tensor(a->src, src_dtype, true) || !ok_tensor(a->dst, a->dtype, true) || !a->freqs) return DTA_ERR_INVALID;
+  RopeParams p{};
+  p.src = t5(a->src); p.dst = t5(a->dst); p.freqs = a->freqs;
+  p.B = a->B; p.T = a->T; p.H = a->H; p.N = a->n_terms; p.HS = a->head_size; p.inverse = a->inverse ? 1 : 0;
+  return status(launch_rope(a->dtype, a->src_f32 != 0, p, (hipStream_t)stream));
+}
+
+int dta_cast_f32(int32_t dtype, int32_t B, int32_t T, int32_t H, int32_t n_terms, int32_t head_size,
+                 const float* src, dta_tensor dst, void* stream) {
+  if (!ok_dims(dtype, B, T, H, n_terms, head_size, 1) || head_size % 8) return DTA_ERR_INVALID;
+  if ((int64_t)B * T == 0) return DTA_OK;
+  if (!aligned_ptr(src) || !ok_tensor(dst, dtype, true)) return DTA_ERR_INVALID;
+  return status(launch_cast(dtype, src, t5(dst), B, T, H, n_terms, head_size, (hipStream_t)stream));
+}
+
+}  // extern "C"

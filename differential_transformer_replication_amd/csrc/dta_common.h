@@ -1,0 +1,169 @@
+// dta_common.h -- shared device helpers for the gfx950 differential-attention
+// kernels: element traits, MFMA fragment I/O, wave reductions.
+//
+// All matrix work uses 32x32 MFMA tiles (64-lane waves):
+//   bf16 / f16 : v_mfma_f32_32x32x16_{bf16,f16}  (K = 16 per instruction)
+//   f32        : v_mfma_f32_32x32x2_f32          (K = 2, exact fp32; parity builds)
+// The C/D accumulator layout is the same for every dtype on gfx950:
+//   lane l, register r  ->  row (r&3) + 8*(r>>2) + 4*(l>>5),  column l&31.
+// A/B operand maps (lane l, half h = l>>5):
+//   16-bit: A[row l&31][k = 8h + j], B[k = 8h + j][col l&31], j = 0..7
+//   f32   : A[row l&31][k = h],      B[k = h][col l&31]
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dta {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+__device__ __forceinline__ int rowof(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+__device__ __forceinline__ float exp2_fast(float x) { return __builtin_amdgcn_exp2f(x); }
+
+__device__ __forceinline__ float wave_max_halves(float v) {
+  // combine lane l with lane l^32 (the two halves that hold the same column)
+  return fmaxf(v, __shfl_xor(v, 32, 64));
+}
+
+template <class E> struct Ops;
+
+// ----------------------------------------------------------- 16-bit types ---
+template <class E, class V8, class V4>
+struct Ops16 {
+  using elem = E;
+  using frag = V8;                    // 8 elements = 4 VGPRs
+  static constexpr int KSTEP = 16;    // k per MFMA
+  static constexpr int KH = 8;        // k elements per lane half
+  static constexpr int VEC = 8;       // elements per 16-byte global access
+
+  __device__ static float to_f(E x) { return (float)x; }
+  __device__ static E from_f(float x) { return (E)x; }
+
+  // A or B operand from a row-major image: row pointer at k = 0.
+  __device__ static frag row(const E* rowp, int s, int h) {
+    return *reinterpret_cast<const frag*>(rowp + s * KSTEP + h * KH);
+  }
+  // 4 rows x 16 columns -> lane i of each 16-lane group gets column i
+  // (ds_read_b64_tr_b16).  base: element (row0, col0) of the 4x(32) strip.
+  __device__ static V4 tr4(const E* base, int stride, int lane) {
+    const int i = lane & 15;
+    const E* p = base + (i >> 2) * stride + ((lane >> 4) & 1) * 16 + (i & 3) * 4;
+    s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p));
+    return __builtin_bit_cast(V4, v);
+  }
+  // Transposed operand whose k order matches an accumulator packed by pack():
+  // element j <-> k row 16s + 8(j>>2) + 4h + (j&3) of the 32-row block at base.
+  __device__ static frag tr_perm(const E* base, int stride, int s, int h, int lane) {
+    V4 lo = tr4(base + (16 * s + 4 * h) * stride, stride, lane);
+    V4 hi = tr4(base + (16 * s + 8 + 4 * h) * stride, stride, lane);
+    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  }
+  // Transposed operand in natural k order: element j <-> k row KSTEP*s + 8h + j.
+  __device__ static frag tr_nat(const E* base, int stride, int s, int h, int lane) {
+    V4 lo = tr4(base + (16 * s + 8 * h) * stride, stride, lane);
+    V4 hi = tr4(base + (16 * s + 8 * h + 4) * stride, stride, lane);
+    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  }
+  // accumulator registers 8s..8s+7 -> operand fragment of k-step s
+  template <int S>
+  __device__ static frag pack(const f32x16& a) {
+    frag f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = (E)a[8 * S + j];
+    return f;
+  }
+  __device__ static frag zero() { return frag{}; }
+  __device__ static frag load_global(const E* p) { return *reinterpret_cast<const frag*>(p); }
+};
+
+template <> struct Ops<__bf16> : Ops16<__bf16, bf16x8, bf16x4> {
+  __device__ static f32x16 mma(frag a, frag b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  }
+};
+template <> struct Ops<_Float16> : Ops16<_Float16, f16x8, f16x4> {
+  __device__ static f32x16 mma(frag a, frag b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+  }
+};
+
+// ------------------------------------------------------------------ fp32 ---
+template <> struct Ops<float> {
+  using elem = float;
+  using frag = float;
+  static constexpr int KSTEP = 2;
+  static constexpr int KH = 1;
+  static constexpr int VEC = 4;
+
+  __device__ static float to_f(float x) { return x; }
+  __device__ static float from_f(float x) { return x; }
+  __device__ static f32x16 mma(float a, float b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+  }
+  __device__ static float row(const float* rowp, int s, int h) { return rowp[2 * s + h]; }
+  __device__ static float tr_perm(const float* base, int stride, int s, int h, int lane) {
+    return base[((s & 3) + 8 * (s >> 2) + 4 * h) * stride + (lane & 31)];
+  }
+  __device__ static float tr_nat(const float* base, int stride, int s, int h, int lane) {
+    return base[(2 * s + h) * stride + (lane & 31)];
+  }
+  template <int S>
+  __device__ static float pack(const f32x16& a) { return a[S]; }
+  __device__ static float zero() { return 0.f; }
+  __device__ static float load_global(const float* p) { return *p; }
+};
+
+// Row padding (in elements) of LDS images.  16-bit: one 16-byte slot, which
+// makes the 32-distinct-row ds_read_b128 pattern conflict-free for every
+// head size; fp32: one element (odd stride) for the scalar reads.
+template <class E> struct Pad { static constexpr int v = 8; };
+template <> struct Pad<float> { static constexpr int v = 1; };
+
+// Copy VEC contiguous elements global -> LDS (zero when !valid).
+template <class E>
+__device__ __forceinline__ void stage_vec(E* dst, const E* src, bool valid) {
+  if constexpr (sizeof(E) == 2) {
+    s16x8 v = valid ? *reinterpret_cast<const s16x8*>(src) : s16x8{};
+    *reinterpret_cast<s16x8*>(dst) = v;     // 16-bit images keep 16-byte aligned rows
+  } else {
+    f32x4 v = valid ? *reinterpret_cast<const f32x4*>(src) : f32x4{};
+    dst[0] = v[0]; dst[1] = v[1]; dst[2] = v[2]; dst[3] = v[3];   // odd-stride rows
+  }
+}
+
+// Store 4 consecutive accumulator values (registers 4g..4g+3) as elements.
+template <class E>
+__device__ __forceinline__ void store4(E* dst, float a, float b, float c, float d) {
+  if constexpr (sizeof(E) == 2) {
+    typedef E v4 __attribute__((ext_vector_type(4)));
+    v4 v = {(E)a, (E)b, (E)c, (E)d};
+    *reinterpret_cast<v4*>(dst) = v;
+  } else {
+    *reinterpret_cast<f32x4*>(dst) = f32x4{a, b, c, d};
+  }
+}
+
+template <class E>
+__device__ __forceinline__ void store4_lds(E* dst, float a, float b, float c, float d) {
+  if constexpr (sizeof(E) == 2) {
+    typedef E v4 __attribute__((ext_vector_type(4)));
+    v4 v = {(E)a, (E)b, (E)c, (E)d};
+    *reinterpret_cast<v4*>(dst) = v;
+  } else {
+    dst[0] = a; dst[1] = b; dst[2] = c; dst[3] = d;
+  }
+}
+
+constexpr float LOG2E = 1.4426950408889634f;
+
+}  // namespace dta

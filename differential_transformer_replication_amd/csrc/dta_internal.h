@@ -1,0 +1,68 @@
+// dta_internal.h -- host-side parameter blocks shared between the C-ABI
+// (dta_capi.cpp) and the per-dtype kernel translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dta {
+
+struct T5 {            // [b][t][h][i] element strides + base pointer
+  void* p;
+  int64_t sb, st, sh, si;
+};
+
+struct FwdParams {
+  T5 q, k, v, o, obr;
+  float* lse;
+  const float* coef;
+  int B, T, H, N, HS, DV;
+  float sl2;           // scale * log2(e)
+};
+
+struct BwdParams {
+  T5 q, k, v, dout, dk, dv;
+  const float* lse;
+  const float* delta;
+  const float* coef;
+  float* dq;           // fp32 [b][t][h][i][d] contiguous
+  int B, T, H, N, HS, DV;
+  float sl2, scale;
+};
+
+// per-dtype launchers (dtype index: 0 bf16, 1 f16, 2 f32); return hipError_t
+int launch_attn_fwd(int dtype, const FwdParams& p, hipStream_t st);
+int launch_attn_bwd(int dtype, const BwdParams& p, hipStream_t st);
+bool attn_supported(int dtype, int hs, int n, int dv);
+
+struct LnParams {
+  int64_t rows, C;
+  float eps, out_scale;
+  const void* x; int64_t xs;
+  void* y; int64_t ys;
+  const float* w; const float* b;
+  float* mean; float* rstd;
+  const void* dy; int64_t dys;
+  void* dx; int64_t dxs;
+  float* dw; float* db;
+};
+
+struct RopeParams {
+  T5 src, dst;
+  const float* freqs;
+  int B, T, H, N, HS;
+  int inverse;
+};
+
+struct DeltaParams {
+  T5 dout, obr;
+  float* delta;
+  int B, T, H, N, DV;
+};
+
+int launch_ln(int dtype, const LnParams& p, bool bwd, hipStream_t st);
+int launch_rope(int dtype, bool src_f32, const RopeParams& p, hipStream_t st);
+int launch_delta(int dtype, const DeltaParams& p, hipStream_t st);
+int launch_dcoef(const float* delta, float* dcoef, int B, int T, int H, int N, hipStream_t st);
+int launch_cast(int dtype, const float* src, const T5& dst, int B, int T, int H, int N, int HS, hipStream_t st);
+
+}  // namespace dta

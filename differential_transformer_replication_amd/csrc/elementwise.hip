@@ -1,0 +1,348 @@
+// elementwise.hip -- HBM-bound kernels around the attention core, gfx950.
+//
+//  * ln_fwd / ln_bwd   GroupLayerNorm over the concatenated heads (C' = H*dv)
+//                      fused with the constant x(1 - 0.8) output scale
+//                      (diff_transformer.py:15-20, 90-91).  One wave per row,
+//                      16-byte vector loads, two-pass mean/variance in registers.
+//  * rope              interleaved-pair rotary embedding of every Q_i / K_i and
+//                      its inverse for the gradients (Ndiff_transformer.py:11-22).
+//  * bwd_delta         delta_i[b,h,t] = <dO, O_i> per row (flash-bwd preprocess);
+//  * dcoef_reduce      dcoef[h][i] = sum_{b,t} delta_i  (d lambda, SURVEY semantic 5).
+//  * cast_f32          fp32 dQ accumulator -> activation dtype.
+#include "dta_common.h"
+#include "dta_internal.h"
+
+namespace dta {
+
+template <class E> struct Vec8;
+template <> struct Vec8<__bf16> { typedef bf16x8 t; };
+template <> struct Vec8<_Float16> { typedef f16x8 t; };
+
+// load/store 8 consecutive elements as fp32
+template <class E>
+__device__ __forceinline__ void ld8(const E* p, float* f) {
+  if constexpr (sizeof(E) == 2) {
+    typename Vec8<E>::t v = *reinterpret_cast<const typename Vec8<E>::t*>(p);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = (float)v[j];
+  } else {
+    f32x4 a = *reinterpret_cast<const f32x4*>(p), b = *reinterpret_cast<const f32x4*>(p + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { f[j] = a[j]; f[j + 4] = b[j]; }
+  }
+}
+template <class E>
+__device__ __forceinline__ void st8(E* p, const float* f) {
+  if constexpr (sizeof(E) == 2) {
+    typename Vec8<E>::t v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (E)f[j];
+    *reinterpret_cast<typename Vec8<E>::t*>(p) = v;
+  } else {
+    *reinterpret_cast<f32x4*>(p) = f32x4{f[0], f[1], f[2], f[3]};
+    *reinterpret_cast<f32x4*>(p + 4) = f32x4{f[4], f[5], f[6], f[7]};
+  }
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+
+// CH = 8-element chunks per lane (C <= 512*CH)
+template <class E, int CH>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(LnParams p) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= p.rows) return;
+  const E* x = reinterpret_cast<const E*>(p.x) + row * p.xs;
+  float v[CH][8];
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int col = (c * 64 + lane) * 8;
+    if (col < p.C) {
+      ld8<E>(x + col, v[c]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += v[c][j];
+    }
+  }
+  const float inv_c = 1.f / (float)p.C;
+  const float mean = wave_sum(s) * inv_c;
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int col = (c * 64 + lane) * 8;
+    if (col < p.C) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { const float d = v[c][j] - mean; ss += d * d; }
+    }
+  }
+  const float var = wave_sum(ss) * inv_c;
+  const float rstd = 1.f / sqrtf(var + p.eps);
+  if (lane == 0) { p.mean[row] = mean; p.rstd[row] = rstd; }
+  E* y = reinterpret_cast<E*>(p.y) + row * p.ys;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int col = (c * 64 + lane) * 8;
+    if (col < p.C) {
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        o[j] = fmaf((v[c][j] - mean) * rstd, p.w[col + j], p.b[col + j]) * p.out_scale;
+      st8<E>(y + col, o);
+    }
+  }
+}
+
+template <class E, int CH>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(LnParams p) {
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  float dwp[CH][8], dbp[CH][8], wv[CH][8];
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int col = (c * 64 + lane) * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      dwp[c][j] = 0.f; dbp[c][j] = 0.f;
+      wv[c][j] = col < p.C ? p.w[col + j] * p.out_scale : 0.f;
+    }
+  }
+  const float inv_c = 1.f / (float)p.C;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + wave; row < p.rows; row += (int64_t)gridDim.x * 4) {
+    const E* x = reinterpret_cast<const E*>(p.x) + row * p.xs;
+    const E* dy = reinterpret_cast<const E*>(p.dy) + row * p.dys;
+    const float mean = p.mean[row], rstd = p.rstd[row];
+    float xh[CH][8], g[CH][8];
+    float sg = 0.f, sgx = 0.f;
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int col = (c * 64 + lane) * 8;
+      if (col < p.C) {
+        float xv[8], dv[8];
+        ld8<E>(x + col, xv);
+        ld8<E>(dy + col, dv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          xh[c][j] = (xv[j] - mean) * rstd;
+          const float dys = dv[j] * p.out_scale;
+          dwp[c][j] = fmaf(dys, xh[c][j], dwp[c][j]);
+          dbp[c][j] += dys;
+          g[c][j] = dv[j] * wv[c][j];
+          sg += g[c][j];
+          sgx = fmaf(g[c][j], xh[c][j], sgx);
+        }
+      }
+    }
+    const float mg = wave_sum(sg) * inv_c, mgx = wave_sum(sgx) * inv_c;
+    E* dx = reinterpret_cast<E*>(p.dx) + row * p.dxs;
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int col = (c * 64 + lane) * 8;
+      if (col < p.C) {
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = rstd * (g[c][j] - mg - xh[c][j] * mgx);
+        st8<E>(dx + col, o);
+      }
+    }
+  }
+  // column partials: reduce the 4 waves through LDS, then one atomic per column per block
+  __shared__ float red[2][4][512];
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int col0 = (c * 64 + lane) * 8;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      red[0][wave][(lane * 8 + j)] = dwp[c][j];
+      red[1][wave][(lane * 8 + j)] = dbp[c][j];
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < 1024; e += 256) {
+      const int which = e >> 9, k = e & 511;
+      const int col = c * 512 + k;
+      if (col < p.C) {
+        const float s = red[which][0][k] + red[which][1][k] + red[which][2][k] + red[which][3][k];
+        atomicAdd((which ? p.db : p.dw) + col, s);
+      }
+    }
+    (void)col0;
+  }
+}
+
+
+// one thread = 4 rotation pairs (8 elements)
+template <class E, class S>
+__global__ __launch_bounds__(256) void rope_kernel(RopeParams p) {
+  const int per_row = p.HS / 8;
+  const int64_t total = (int64_t)p.B * p.T * p.H * p.N * per_row;
+  for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * 256) {
+    int64_t r = idx;
+    const int c = r % per_row; r /= per_row;
+    const int i = r % p.N; r /= p.N;
+    const int h = r % p.H; r /= p.H;
+    const int t = r % p.T; const int b = (int)(r / p.T);
+    const S* src = reinterpret_cast<const S*>(p.src.p) + b * p.src.sb + (int64_t)t * p.src.st + h * p.src.sh + i * p.src.si + c * 8;
+    E* dst = reinterpret_cast<E*>(p.dst.p) + b * p.dst.sb + (int64_t)t * p.dst.st + h * p.dst.sh + i * p.dst.si + c * 8;
+    float x[8], o[8];
+    ld8<S>(src, x);
+    const float* f = p.freqs + ((int64_t)t * (p.HS / 2) + c * 4) * 2;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float cs = f[2 * j], sn = p.inverse ? -f[2 * j + 1] : f[2 * j + 1];
+      const float a = x[2 * j], bb = x[2 * j + 1];
+      o[2 * j] = a * cs - bb * sn;          // (a + ib)(cos + i sin)
+      o[2 * j + 1] = a * sn + bb * cs;
+    }
+    st8<E>(dst, o);
+  }
+}
+
+
+// one group of G = DV/8 lanes per (b, t, h) row; each lane one 16-byte vector
+template <class E>
+__global__ __launch_bounds__(256) void bwd_delta_kernel(DeltaParams p) {
+  const int G = p.DV / 8;                       // lanes per row (<= 64)
+  const int lane = threadIdx.x & 63;
+  const int rows_per_wave = 64 / G;
+  const int64_t nrows = (int64_t)p.B * p.T * p.H;
+  const int64_t wave_id = ((int64_t)blockIdx.x * 256 + threadIdx.x) / 64;
+  const int64_t row = wave_id * rows_per_wave + lane / G;
+  const int sub = lane % G;
+  const bool ok = row < nrows;
+  const int h = ok ? (int)(row % p.H) : 0;
+  const int t = ok ? (int)((row / p.H) % p.T) : 0;
+  const int b = ok ? (int)(row / ((int64_t)p.H * p.T)) : 0;
+  float dov[8];
+  if (ok) ld8<E>(reinterpret_cast<const E*>(p.dout.p) + b * p.dout.sb + (int64_t)t * p.dout.st + h * p.dout.sh + sub * 8, dov);
+  for (int i = 0; i < p.N; ++i) {
+    float s = 0.f;
+    if (ok) {
+      float ov[8];
+      ld8<E>(reinterpret_cast<const E*>(p.obr.p) + i * p.obr.si + b * p.obr.sb + (int64_t)t * p.obr.st + h * p.obr.sh + sub * 8, ov);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s = fmaf(dov[j], ov[j], s);
+    }
+    for (int o = G / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if (ok && sub == 0) p.delta[(((int64_t)i * p.B + b) * p.H + h) * p.T + t] = s;
+  }
+}
+
+// dcoef[h][i] = sum over b, t of delta[i][b][h][t]; one block per (h, i)
+__global__ __launch_bounds__(256) void dcoef_kernel(const float* delta, float* dcoef, int B, int T, int H, int N) {
+  const int h = blockIdx.x / N, i = blockIdx.x % N;
+  float s = 0.f;
+  for (int b = 0; b < B; ++b) {
+    const float* d = delta + (((int64_t)i * B + b) * H + h) * T;
+    for (int t = threadIdx.x; t < T; t += 256) s += d[t];
+  }
+  s = wave_sum(s);
+  __shared__ float part[4];
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) dcoef[h * N + i] = part[0] + part[1] + part[2] + part[3];
+}
+
+template <class E>
+__global__ __launch_bounds__(256) void cast_f32_kernel(const float* src, T5 dst, int B, int T, int H, int N, int HS) {
+  const int per_row = HS / 8;
+  const int64_t total = (int64_t)B * T * H * N * per_row;
+  for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * 256) {
+    int64_t r = idx;
+    const int c = r % per_row; r /= per_row;
+    const int i = r % N; r /= N;
+    const int h = r % H; r /= H;
+    const int t = r % T; const int b = (int)(r / T);
+    float v[8];
+    ld8<float>(src + idx * 8, v);
+    st8<E>(reinterpret_cast<E*>(dst.p) + b * dst.sb + (int64_t)t * dst.st + h * dst.sh + i * dst.si + c * 8, v);
+  }
+}
+
+// ---------------------------------------------------------------- hosts ---
+static inline int grid_for(int64_t items) {
+  int64_t g = (items + 255) / 256;
+  return (int)(g > 16384 ? 16384 : (g < 1 ? 1 : g));
+}
+
+template <class E>
+int ln_launch(const LnParams& p, bool bwd, hipStream_t st) {
+  const int64_t ch = (p.C + 511) / 512;
+  const int fwd_grid = (int)((p.rows + 3) / 4);
+  const int bwd_grid = (int)std::min<int64_t>((p.rows + 3) / 4, 2048);
+#define DTA_LN(CH_)                                                                    \
+  if (ch <= CH_) {                                                                     \
+    if (bwd) hipLaunchKernelGGL((ln_bwd_kernel<E, CH_>), dim3(bwd_grid), dim3(256), 0, st, p); \
+    else hipLaunchKernelGGL((ln_fwd_kernel<E, CH_>), dim3(fwd_grid), dim3(256), 0, st, p);     \
+    return (int)hipGetLastError();                                                     \
+  }
+  DTA_LN(1) DTA_LN(2) DTA_LN(4) DTA_LN(8) DTA_LN(16)
+#undef DTA_LN
+  return -2;
+}
+
+int launch_ln(int dtype, const LnParams& p, bool bwd, hipStream_t st) {
+  if (p.rows == 0) return 0;
+  switch (dtype) {
+    case 0: return ln_launch<__bf16>(p, bwd, st);
+    case 1: return ln_launch<_Float16>(p, bwd, st);
+    case 2: return ln_launch<float>(p, bwd, st);
+  }
+  return -2;
+}
+
+int launch_rope(int dtype, bool src_f32, const RopeParams& p, hipStream_t st) {
+  const int64_t items = (int64_t)p.B * p.T * p.H * p.N * (p.HS / 8);
+  if (items == 0) return 0;
+  dim3 g(grid_for(items));
+#define DTA_R(E_)                                                                         \
+  if (src_f32) hipLaunchKernelGGL((rope_kernel<E_, float>), g, dim3(256), 0, st, p);       \
+  else hipLaunchKernelGGL((rope_kernel<E_, E_>), g, dim3(256), 0, st, p);
+  switch (dtype) {
+    case 0: DTA_R(__bf16) break;
+    case 1: DTA_R(_Float16) break;
+    case 2: DTA_R(float) break;
+    default: return -2;
+  }
+#undef DTA_R
+  return (int)hipGetLastError();
+}
+
+int launch_delta(int dtype, const DeltaParams& p, hipStream_t st) {
+  const int64_t nrows = (int64_t)p.B * p.T * p.H;
+  if (nrows == 0) return 0;
+  const int rows_per_wave = 64 / (p.DV / 8);
+  const int64_t waves = (nrows + rows_per_wave - 1) / rows_per_wave;
+  dim3 g((unsigned)((waves + 3) / 4));
+  switch (dtype) {
+    case 0: hipLaunchKernelGGL(bwd_delta_kernel<__bf16>, g, dim3(256), 0, st, p); break;
+    case 1: hipLaunchKernelGGL(bwd_delta_kernel<_Float16>, g, dim3(256), 0, st, p); break;
+    case 2: hipLaunchKernelGGL(bwd_delta_kernel<float>, g, dim3(256), 0, st, p); break;
+    default: return -2;
+  }
+  return (int)hipGetLastError();
+}
+
+int launch_dcoef(const float* delta, float* dcoef, int B, int T, int H, int N, hipStream_t st) {
+  hipLaunchKernelGGL(dcoef_kernel, dim3(H * N), dim3(256), 0, st, delta, dcoef, B, T, H, N);
+  return (int)hipGetLastError();
+}
+
+int launch_cast(int dtype, const float* src, const T5& dst, int B, int T, int H, int N, int HS, hipStream_t st) {
+  const int64_t items = (int64_t)B * T * H * N * (HS / 8);
+  if (items == 0) return 0;
+  dim3 g(grid_for(items));
+  switch (dtype) {
+    case 0: hipLaunchKernelGGL(cast_f32_kernel<__bf16>, g, dim3(256), 0, st, src, dst, B, T, H, N, HS); break;
+    case 1: hipLaunchKernelGGL(cast_f32_kernel<_Float16>, g, dim3(256), 0, st, src, dst, B, T, H, N, HS); break;
+    case 2: hipLaunchKernelGGL(cast_f32_kernel<float>, g, dim3(256), 0, st, src, dst, B, T, H, N, HS); break;
+    default: return -2;
+  }
+  return (int)hipGetLastError();
+}
+
+}  // namespace dta

@@ -1,0 +1,202 @@
+"""Drop-in replacement of the reference ``diff_transformer.py`` module surface.
+
+Class names, constructor arguments, forward signatures, parameter/buffer names
+(hence ``state_dict`` keys) and parameter-creation order (hence seeded
+initialisation) follow the reference (``/root/reference/diff_transformer.py``).
+What changes is the execution: the per-head Python loop of eager ATen ops
+(diff_transformer.py:89, 50-73) becomes one packed projection GEMM, one fused
+HIP attention launch for all heads (``ops.diff_attention``) and one fused
+GroupLayerNorm x0.2 launch (``ops.group_ln_scale``).  SwiGLU, Block and the
+model shell are carried as plain PyTorch.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+from torch.nn import functional as F
+
+from . import ops
+from ._compat import (emit_tril_hooks, lambda_init_value, check_seq_len, check_dropout, fill_if_changed,
+                      mha_out_scale)
+
+__all__ = ["GroupLayerNorm", "DiffHead", "MultiHeadDiffAttention", "SwiGLU", "Block", "DiffTransformer"]
+
+
+class GroupLayerNorm(nn.Module):
+    """LayerNorm over the concatenated width num_heads*2*head_dim -- not per head,
+    not RMS (diff_transformer.py:5-20, SURVEY semantic 1)."""
+
+    def __init__(self, num_heads, head_dim):
+        super().__init__()
+        self.eps = 1e-5
+        self.num_heads = num_heads
+        self.head_dim = head_dim * 2
+        width = num_heads * self.head_dim
+        self.weight = nn.Parameter(torch.ones(1, 1, width))
+        self.bias = nn.Parameter(torch.zeros(1, 1, width))
+
+    def forward(self, x):
+        return ops.group_ln_scale(x, self.weight, self.bias, self.eps, 1.0)
+
+
+def _layer_lambda_coef(lq1, lk1, lq2, lk2, init: torch.Tensor) -> torch.Tensor:
+    """(H, 2) signed branch weights [1, -lambda_h] with
+    lambda = mean(exp(lq1*lk1) - exp(lq2*lk2) + init)  (diff_transformer.py:41-48, 70)."""
+    lam = (torch.exp(lq1 * lk1) - torch.exp(lq2 * lk2) + init).mean(dim=-1)
+    return torch.stack([torch.ones_like(lam), -lam], dim=-1)
+
+
+class DiffHead(nn.Module):
+    """One differential-attention head (diff_transformer.py:22-73)."""
+
+    def __init__(self, head_size, n_embd, dropout, block_size):
+        super().__init__()
+        # creation order = reference order (seeded init parity)
+        self.key1 = nn.Linear(n_embd, head_size, bias=False)
+        self.query1 = nn.Linear(n_embd, head_size, bias=False)
+        self.key2 = nn.Linear(n_embd, head_size, bias=False)
+        self.query2 = nn.Linear(n_embd, head_size, bias=False)
+        self.value = nn.Linear(n_embd, head_size * 2, bias=False)
+        self.block_size = block_size
+        self.head_size = head_size
+        emit_tril_hooks(self, block_size)          # virtual `tril` buffer (SURVEY semantic 8)
+        self.dropout = nn.Dropout(dropout)
+        self.lambda_q1 = nn.Parameter(torch.zeros(head_size))
+        self.lambda_k1 = nn.Parameter(torch.zeros(head_size))
+        self.lambda_q2 = nn.Parameter(torch.zeros(head_size))
+        self.lambda_k2 = nn.Parameter(torch.zeros(head_size))
+        self.register_buffer("lambda_init", torch.tensor(0.8))
+
+    def get_lambda(self, layer_idx):
+        """diff_transformer.py:41-48, including the buffer side effect (:44)."""
+        init = lambda_init_value(layer_idx, self.lambda_init)
+        fill_if_changed(self.lambda_init, init)
+        lam = torch.exp(self.lambda_q1 * self.lambda_k1) - torch.exp(self.lambda_q2 * self.lambda_k2) \
+            + self.lambda_init
+        return lam.mean()
+
+    def packed_weight(self) -> torch.Tensor:
+        """Rows in the kernel's packed order [Q (N=2, hs) | K (2, hs) | V (2hs)] for H=1."""
+        return torch.cat([self.query1.weight, self.query2.weight, self.key1.weight, self.key2.weight,
+                          self.value.weight], dim=0)
+
+    def forward(self, x, layer_idx):
+        check_seq_len(x.shape[1], self.block_size)
+        check_dropout(self.dropout, self.training)
+        init = lambda_init_value(layer_idx, self.lambda_init)
+        fill_if_changed(self.lambda_init, init)
+        coef = _layer_lambda_coef(self.lambda_q1[None].float(), self.lambda_k1[None].float(),
+                                  self.lambda_q2[None].float(), self.lambda_k2[None].float(), init)
+        qkv = F.linear(x, self.packed_weight())
+        return ops.diff_attention(qkv, coef, 1, 2, self.head_size)
+
+
+class MultiHeadDiffAttention(nn.Module):
+    """All heads in one fused launch (diff_transformer.py:75-93)."""
+
+    def __init__(self, num_heads, head_size, n_embd, dropout, block_size):
+        super().__init__()
+        self.heads = nn.ModuleList([DiffHead(head_size, n_embd, dropout, block_size) for _ in range(num_heads)])
+        self.group_norm = GroupLayerNorm(num_heads, head_size)
+        self.proj = nn.Linear(head_size * 2 * num_heads, n_embd)
+        self.dropout = nn.Dropout(dropout)
+        self.register_buffer("lambda_init", torch.tensor(0.8))
+        self.num_heads = num_heads
+        self.head_size = head_size
+        self.block_size = block_size
+
+    def packed_weight(self) -> torch.Tensor:
+        hs = self.heads
+        q = [w for h in hs for w in (h.query1.weight, h.query2.weight)]
+        k = [w for h in hs for w in (h.key1.weight, h.key2.weight)]
+        v = [h.value.weight for h in hs]
+        return torch.cat(q + k + v, dim=0)
+
+    def coefficients(self, layer_idx) -> torch.Tensor:
+        init = lambda_init_value(layer_idx, self.heads[0].lambda_init)
+        for h in self.heads:                       # get_lambda's buffer side effect, every head
+            fill_if_changed(h.lambda_init, init)
+        st = lambda name: torch.stack([getattr(h, name) for h in self.heads]).float()
+        return _layer_lambda_coef(st("lambda_q1"), st("lambda_k1"), st("lambda_q2"), st("lambda_k2"), init)
+
+    def forward(self, x, layer_idx):
+        check_seq_len(x.shape[1], self.block_size)
+        for h in self.heads:
+            check_dropout(h.dropout, self.training)
+        coef = self.coefficients(layer_idx)
+        qkv = F.linear(x, self.packed_weight())
+        out = ops.diff_attention(qkv, coef, self.num_heads, 2, self.head_size)
+        # GroupLayerNorm then x(1 - lambda_init) with the MHA's own, never-updated 0.8 buffer
+        gn = self.group_norm
+        out = ops.group_ln_scale(out, gn.weight, gn.bias, gn.eps, mha_out_scale(self.lambda_init))
+        return self.dropout(self.proj(out))
+
+
+class SwiGLU(nn.Module):
+    """silu(W_g x) * (W_x x)  (diff_transformer.py:95-105)."""
+
+    def __init__(self, size_in, size_out):
+        super().__init__()
+        self.linear_gate = nn.Linear(size_in, size_out)
+        self.linear_xform = nn.Linear(size_in, size_out)
+
+    def forward(self, x):
+        return F.silu(self.linear_gate(x)) * self.linear_xform(x)
+
+
+class Block(nn.Module):
+    """Pre-LN residual block (diff_transformer.py:107-126)."""
+
+    def __init__(self, n_embd, n_head, block_size, dropout):
+        super().__init__()
+        head_size = n_embd // (n_head * 2)
+        self.diff_attn = MultiHeadDiffAttention(n_head, head_size, n_embd, dropout, block_size)
+        self.ffwd = nn.Sequential(SwiGLU(n_embd, 4 * n_embd), nn.Linear(4 * n_embd, n_embd), nn.Dropout(dropout))
+        self.ln1 = nn.LayerNorm(n_embd)
+        self.ln2 = nn.LayerNorm(n_embd)
+
+    def forward(self, x, layer_idx):
+        x = x + self.diff_attn(self.ln1(x), layer_idx)
+        return x + self.ffwd(self.ln2(x))
+
+
+class DiffTransformer(nn.Module):
+    """Token + position embeddings, Block x n_layer, ln_f, lm_head, CE loss
+    (diff_transformer.py:128-185)."""
+
+    def __init__(self, vocab_size, n_embd, n_head, n_layer, block_size, dropout):
+        super().__init__()
+        self.block_size = block_size
+        self.token_embedding_table = nn.Embedding(vocab_size, n_embd)
+        self.position_embedding_table = nn.Embedding(block_size, n_embd)
+        self.blocks = nn.ModuleList([Block(n_embd, n_head, block_size, dropout) for _ in range(n_layer)])
+        self.ln_f = nn.LayerNorm(n_embd)
+        self.lm_head = nn.Linear(n_embd, vocab_size)
+        self.apply(self._init_weights)
+
+    def _init_weights(self, module):
+        if isinstance(module, (nn.Linear, nn.Embedding)):
+            nn.init.normal_(module.weight, mean=0.0, std=0.02)
+            if isinstance(module, nn.Linear) and module.bias is not None:
+                nn.init.zeros_(module.bias)
+
+    def forward(self, idx, targets=None):
+        B, T = idx.shape
+        pos = torch.arange(T, device=idx.device)
+        x = self.token_embedding_table(idx) + self.position_embedding_table(pos)
+        for layer, block in enumerate(self.blocks, 1):     # 1-based layer index (:161)
+            x = block(x, layer)
+        logits = self.lm_head(self.ln_f(x))
+        loss = None
+        if targets is not None:
+            loss = F.cross_entropy(logits.view(B * T, -1), targets.view(B * T))
+        return logits, loss
+
+    @torch.no_grad()
+    def generate(self, idx, max_new_tokens):
+        """Naive sampling: full forward per token, cropped to block_size (:177-185)."""
+        for _ in range(max_new_tokens):
+            logits, _ = self(idx[:, -self.block_size:])
+            probs = F.softmax(logits[:, -1, :], dim=-1)
+            idx = torch.cat((idx, torch.multinomial(probs, num_samples=1)), dim=1)
+        return idx

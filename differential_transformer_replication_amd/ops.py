@@ -1,0 +1,179 @@
+"""torch.autograd.Function wrappers over the C ABI (the only compute path).
+
+``diff_attention(qkv, coef, ...)``
+    Fused N-branch causal differential attention over a packed projection
+    output ``qkv`` of shape (B, T, W), W = 2*H*N*hs + H*dv, laid out
+    ``[Q (H, N, hs) | K (H, N, hs) | V (H, dv)]``.  Returns O of shape
+    (B, T, H*dv) = concatenated per-head outputs (diff_transformer.py:89, before
+    the GroupLayerNorm).  Backward writes dQ/dK/dV into one (B, T, W) buffer, so
+    the projection GEMM's backward sees a single gradient tensor.
+``group_ln_scale(x, w, b, eps, out_scale)``
+    GroupLayerNorm over the last dim fused with the constant output scale
+    (diff_transformer.py:15-20, 90-91).
+
+There is no CPU or eager fallback: non-CUDA tensors raise.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+
+from . import _lib
+
+Tensor = torch.Tensor
+
+
+def _require_gpu(*ts: Tensor) -> None:
+    for t in ts:
+        if t is not None and t.device.type != "cuda":
+            raise RuntimeError("differential_transformer_replication_amd ops run only on the MI355X "
+                               "HIP path (libdiffattn.so); got a tensor on " + str(t.device))
+
+
+def packed_width(H: int, N: int, hs: int, dv: int) -> int:
+    return 2 * H * N * hs + H * dv
+
+
+def split_packed(qkv: Tensor, H: int, N: int, hs: int, dv: int):
+    """Strided (B,T,H,N,hs)/(B,T,H,dv) views of the packed projection output."""
+    B, T, W = qkv.shape
+    nq = H * N * hs
+    q = qkv[..., :nq].unflatten(-1, (H, N, hs))
+    k = qkv[..., nq:2 * nq].unflatten(-1, (H, N, hs))
+    v = qkv[..., 2 * nq:].unflatten(-1, (H, dv))
+    return q, k, v
+
+
+class _DiffAttention(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv: Tensor, coef: Tensor, H: int, N: int, hs: int, freqs: Optional[Tensor]):
+        lib = _lib.load()
+        _require_gpu(qkv, coef)
+        if qkv.dim() != 3:
+            raise RuntimeError("qkv must be (B, T, W)")
+        qkv = qkv.contiguous()
+        B, T, W = qkv.shape
+        dv = 2 * hs
+        if W != packed_width(H, N, hs, dv):
+            raise RuntimeError(f"packed width {W} != 2*H*N*hs + H*dv = {packed_width(H, N, hs, dv)}")
+        dt = _lib.dtype_code(qkv.dtype)
+        if not lib.dta_supported(dt, hs, N, dv):
+            raise RuntimeError(f"no gfx950 kernel for head_size={hs}, n_terms={N}, dtype={qkv.dtype}")
+        coef = coef.detach().to(torch.float32).contiguous()
+        dev = qkv.device
+        stream = _lib.stream_handle(dev)
+        q, k, v = split_packed(qkv, H, N, hs, dv)
+        qk_rot = None
+        if freqs is not None:
+            # RoPE of every Q_i/K_i (Ndiff_transformer.py:104-109): [Q|K] viewed as 2H heads
+            qk_rot = torch.empty(B, T, 2 * H, N, hs, device=dev, dtype=qkv.dtype)
+            src = qkv[..., :2 * H * N * hs].unflatten(-1, (2 * H, N, hs))
+            ra = _lib.RopeArgs(dt, B, T, 2 * H, N, hs, 0, 0, _lib.tensor5(src), _lib.tensor5(qk_rot),
+                               freqs.data_ptr())
+            _lib.check(lib.dta_rope(ra, stream))
+            q, k = qk_rot[:, :, :H], qk_rot[:, :, H:]
+        o = torch.empty(B, T, H, dv, device=dev, dtype=qkv.dtype)
+        obr = torch.empty(N, B, T, H, dv, device=dev, dtype=qkv.dtype)
+        lse = torch.empty(N, B, H, T, device=dev, dtype=torch.float32)
+        obr_t = _lib.DtaTensor(obr.data_ptr(), *obr.stride()[1:4], obr.stride(0))
+        a = _lib.AttnFwdArgs(dt, B, T, H, N, hs, dv, 1.0 / math.sqrt(hs), 0.0,
+                             _lib.tensor5(q), _lib.tensor5(k), _lib.tensor5(v), _lib.tensor5(o), obr_t,
+                             lse.data_ptr(), coef.data_ptr())
+        _lib.check(lib.dta_attn_fwd(a, stream))
+        ctx.save_for_backward(qkv, qk_rot, obr, lse, coef, freqs)
+        ctx.dims = (H, N, hs, dv)
+        return o.view(B, T, H * dv)
+
+    @staticmethod
+    def backward(ctx, do: Tensor):
+        lib = _lib.load()
+        qkv, qk_rot, obr, lse, coef, freqs = ctx.saved_tensors
+        H, N, hs, dv = ctx.dims
+        B, T, W = qkv.shape
+        dev = qkv.device
+        stream = _lib.stream_handle(dev)
+        dt = _lib.dtype_code(qkv.dtype)
+        do = do.to(qkv.dtype).contiguous().view(B, T, H, dv)
+        q, k, v = split_packed(qkv, H, N, hs, dv)
+        if qk_rot is not None:
+            q, k = qk_rot[:, :, :H], qk_rot[:, :, H:]
+        dqkv = torch.empty_like(qkv)
+        dq, dk, dvv = split_packed(dqkv, H, N, hs, dv)
+        dcoef = torch.empty(H, N, device=dev, dtype=torch.float32)
+        delta = torch.empty(N, B, H, T, device=dev, dtype=torch.float32)
+        dq32 = torch.empty(B, T, H, N, hs, device=dev, dtype=torch.float32)
+        rope = freqs is not None
+        dk_rot = torch.empty(B, T, H, N, hs, device=dev, dtype=qkv.dtype) if rope else None
+        obr_t = _lib.DtaTensor(obr.data_ptr(), *obr.stride()[1:4], obr.stride(0))
+        null = _lib.DtaTensor(None, 0, 0, 0, 0)
+        a = _lib.AttnBwdArgs(dt, B, T, H, N, hs, dv, 1.0 / math.sqrt(hs), 0.0,
+                             _lib.tensor5(q), _lib.tensor5(k), _lib.tensor5(v), obr_t,
+                             lse.data_ptr(), coef.data_ptr(), _lib.tensor5(do),
+                             null if rope else _lib.tensor5(dq),
+                             _lib.tensor5(dk_rot if rope else dk), _lib.tensor5(dvv),
+                             dcoef.data_ptr(), delta.data_ptr(), dq32.data_ptr())
+        _lib.check(lib.dta_attn_bwd(a, stream))
+        if rope:
+            # gradients back through the rotation: conjugate rotate (Ndiff_transformer.py:11-22 bwd)
+            ra = _lib.RopeArgs(dt, B, T, H, N, hs, 1, 1, _lib.tensor5(dq32), _lib.tensor5(dq), freqs.data_ptr())
+            _lib.check(lib.dta_rope(ra, stream))
+            ra = _lib.RopeArgs(dt, B, T, H, N, hs, 1, 0, _lib.tensor5(dk_rot), _lib.tensor5(dk), freqs.data_ptr())
+            _lib.check(lib.dta_rope(ra, stream))
+        return dqkv, dcoef, None, None, None, None
+
+
+def diff_attention(qkv: Tensor, coef: Tensor, H: int, N: int, hs: int,
+                   freqs: Optional[Tensor] = None) -> Tensor:
+    """O = sum_i coef[h,i] softmax_causal(Q_i K_i^T/sqrt(hs)) V for every head.
+
+    ``freqs``: fp32 (T, hs/2, 2) rotary table (view_as_real of freqs_cis[:T]) or None.
+    """
+    if freqs is not None:
+        freqs = freqs.to(device=qkv.device, dtype=torch.float32).contiguous()
+    return _DiffAttention.apply(qkv, coef, H, N, hs, freqs)
+
+
+class _GroupLNScale(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x: Tensor, w: Tensor, b: Tensor, eps: float, out_scale: float):
+        lib = _lib.load()
+        _require_gpu(x, w, b)
+        C = x.shape[-1]
+        x2 = x.contiguous().view(-1, C)
+        rows = x2.shape[0]
+        w32 = w.detach().to(torch.float32).contiguous().view(-1)
+        b32 = b.detach().to(torch.float32).contiguous().view(-1)
+        if w32.numel() != C or b32.numel() != C:
+            raise RuntimeError("GroupLayerNorm weight/bias size must equal the normalised width")
+        y = torch.empty_like(x2)
+        mean = torch.empty(rows, device=x.device, dtype=torch.float32)
+        rstd = torch.empty_like(mean)
+        a = _lib.LnArgs(_lib.dtype_code(x.dtype), rows, C, eps, out_scale, x2.data_ptr(), C, y.data_ptr(), C,
+                        w32.data_ptr(), b32.data_ptr(), mean.data_ptr(), rstd.data_ptr(), None, 0, None, 0,
+                        None, None)
+        _lib.check(lib.dta_ln_fwd(a, _lib.stream_handle(x.device)))
+        ctx.save_for_backward(x2, w32, mean, rstd)
+        ctx.meta = (eps, out_scale, x.shape, w.dtype, w.shape, b.dtype, b.shape)
+        return y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dy: Tensor):
+        lib = _lib.load()
+        x2, w32, mean, rstd = ctx.saved_tensors
+        eps, out_scale, xshape, wdt, wshape, bdt, bshape = ctx.meta
+        C = x2.shape[1]
+        dy2 = dy.to(x2.dtype).contiguous().view(-1, C)
+        dx = torch.empty_like(x2)
+        dw = torch.zeros(C, device=x2.device, dtype=torch.float32)
+        db = torch.zeros(C, device=x2.device, dtype=torch.float32)
+        a = _lib.LnArgs(_lib.dtype_code(x2.dtype), x2.shape[0], C, eps, out_scale, x2.data_ptr(), C, None, 0,
+                        w32.data_ptr(), None, mean.data_ptr(), rstd.data_ptr(), dy2.data_ptr(), C,
+                        dx.data_ptr(), C, dw.data_ptr(), db.data_ptr())
+        _lib.check(lib.dta_ln_bwd(a, _lib.stream_handle(x2.device)))
+        return dx.view(xshape), dw.to(wdt).view(wshape), db.to(bdt).view(bshape), None, None
+
+
+def group_ln_scale(x: Tensor, w: Tensor, b: Tensor, eps: float = 1e-5, out_scale: float = 1.0) -> Tensor:
+    return _GroupLNScale.apply(x, w, b, eps, out_scale)

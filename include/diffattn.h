@@ -1,0 +1,156 @@
+/*
+ * diffattn.h -- C ABI of libdiffattn.so, the MI355X (gfx950) differential
+ * attention library.
+ *
+ * The reference (JoshFCooper415/differential_transformer_replication) has no
+ * native code, plugin or FFI: its hot path is eager ATen called from
+ * nn.Module.forward.  Each entry point below replaces a group of those eager
+ * ops; the comment on each cites the reference lines it replaces.  The Python
+ * package binds these through ctypes (differential_transformer_replication_amd/
+ * _lib.py); INTEGRATION.md shows the binding a maintainer would add.
+ *
+ * Conventions
+ *  - Plain C types only: device pointers, element strides (int64, in
+ *    ELEMENTS not bytes), sizes, a hipStream_t passed as void*.
+ *  - The caller (PyTorch's caching allocator) owns every buffer.  The library
+ *    never allocates or frees device memory and keeps no state.
+ *  - Every launch is asynchronous on the given stream; no host sync.
+ *  - Functions return DTA_OK (0) or a negative error code and never throw
+ *    across the ABI; dta_error_string() describes a code.
+ *  - dtype applies to Q/K/V/O/dO/dQ/dK/dV activations; LSE, delta, the
+ *    coefficients, the LayerNorm statistics/parameters and every *_f32 buffer
+ *    are always fp32.
+ *
+ * Layouts (element strides are given per tensor so strided views of one
+ * packed projection output can be passed without copies):
+ *   Q, K   [b][t][h][i][d]   i < n_terms (the N softmax branches), d < head_size
+ *   V, O   [b][t][h][e]      e < dv (dv = 2*head_size for diff attention)
+ *   Obr    [i][b][t][h][e]   per-branch normalised outputs A_i V (saved for bwd)
+ *   LSE    [i][b][h][t]      fp32, log2-sum-exp of the scaled scores
+ *   coef   [h][i]            fp32, signed branch weights (diff: [1, -lambda];
+ *                            N-diff: [+l0, -l1, +l2, ...])
+ */
+#ifndef DIFFATTN_H_
+#define DIFFATTN_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DTA_ABI_VERSION 1
+
+enum dta_dtype { DTA_BF16 = 0, DTA_F16 = 1, DTA_F32 = 2 };
+
+enum dta_status {
+  DTA_OK = 0,
+  DTA_ERR_INVALID = -1,      /* bad shape / stride / pointer / argument   */
+  DTA_ERR_UNSUPPORTED = -2,  /* head_size / n_terms / dtype not built     */
+  DTA_ERR_LAUNCH = -3,       /* hipLaunch / hipMemsetAsync failed         */
+  DTA_ERR_DROPOUT = -4       /* attention dropout p > 0 is not supported  */
+};
+
+typedef struct dta_tensor {
+  void* ptr;
+  int64_t sb, st, sh, si;    /* strides for [b][t][h][i]; si unused for V/O */
+} dta_tensor;
+
+/* Forward of the fused N-branch causal differential attention core.
+ * Replaces, for all heads at once, DiffHead.forward's scores/mask/softmax/
+ * dropout/combine/@V (diff_transformer.py:57-72), the per-head loop
+ * (diff_transformer.py:89) and AlternatingDiffHead's branch loop
+ * (Ndiff_transformer.py:102-125; RoPE is applied beforehand by dta_rope).
+ * O = sum_i coef[h][i] * softmax(mask(Q_i K_i^T / sqrt(hs))) V. */
+typedef struct dta_attn_fwd_args {
+  int32_t dtype;             /* enum dta_dtype */
+  int32_t B, T, H, n_terms, head_size, dv;
+  float scale;               /* 1/sqrt(head_size) (diff_transformer.py:57) */
+  float dropout_p;           /* must be 0 */
+  dta_tensor q, k, v;        /* inputs */
+  dta_tensor o;              /* output, combined */
+  dta_tensor obr;            /* output [i][b][t][h][e]: sb,st,sh,si = strides of b,t,h,i */
+  float* lse;                /* output fp32 [i][b][h][t], contiguous */
+  const float* coef;         /* fp32 [h][i], contiguous */
+} dta_attn_fwd_args;
+
+int dta_attn_fwd(const dta_attn_fwd_args* a, void* stream);
+
+/* Backward of dta_attn_fwd (the autograd of diff_transformer.py:57-72 and
+ * Ndiff_transformer.py:102-125): dQ_i, dK_i, dV and d(coef).  Maps are
+ * recomputed from LSE; nothing T x T is stored.  dcoef[h][i] =
+ * sum_{b,t} <dO, A_i V> (SURVEY semantic 5), from which autograd reaches
+ * lambda_q and lambda_k params through get_lambda (diff_transformer.py:41-48).
+ * Workspaces (caller-allocated, see dta_attn_bwd_workspace_bytes):
+ *   delta   fp32 [i][b][h][t]
+ *   dq_f32  fp32 [b][t][h][i][d] contiguous (zeroed by the call) */
+typedef struct dta_attn_bwd_args {
+  int32_t dtype;
+  int32_t B, T, H, n_terms, head_size, dv;
+  float scale;
+  float dropout_p;
+  dta_tensor q, k, v, obr;
+  const float* lse;          /* fp32 [i][b][h][t] from the forward */
+  const float* coef;         /* fp32 [h][i] */
+  dta_tensor dout;           /* dO [b][t][h][e] */
+  dta_tensor dq, dk, dv_out; /* outputs (dtype); dq is written from dq_f32 */
+  float* dcoef;              /* output fp32 [h][i] (overwritten) */
+  float* delta;              /* workspace fp32 [i][b][h][t] */
+  float* dq_f32;             /* workspace fp32 [b][t][h][i][d] */
+} dta_attn_bwd_args;
+
+int dta_attn_bwd(const dta_attn_bwd_args* a, void* stream);
+size_t dta_attn_bwd_workspace_bytes(int32_t B, int32_t T, int32_t H, int32_t n_terms,
+                                    int32_t head_size);
+
+/* Cross-head LayerNorm x out_scale (GroupLayerNorm.forward,
+ * diff_transformer.py:15-20, then `out * (1 - self.lambda_init)`,
+ * diff_transformer.py:90-91; same at Ndiff_transformer.py:33-38,145-146).
+ * Rows of width C; y = ((x - mean) * rstd * w + b) * out_scale.
+ * mean/rstd (fp32 [rows]) are saved for dta_ln_bwd. */
+typedef struct dta_ln_args {
+  int32_t dtype;
+  int64_t rows, C;
+  float eps, out_scale;
+  const void* x; int64_t x_stride;   /* row stride, elements */
+  void* y; int64_t y_stride;
+  const float* w; const float* b;    /* fp32 [C] */
+  float* mean; float* rstd;          /* fp32 [rows] */
+  /* backward only */
+  const void* dy; int64_t dy_stride;
+  void* dx; int64_t dx_stride;
+  float* dw; float* db;              /* fp32 [C], accumulated (caller zeroes) */
+} dta_ln_args;
+
+int dta_ln_fwd(const dta_ln_args* a, void* stream);
+int dta_ln_bwd(const dta_ln_args* a, void* stream);
+
+/* Interleaved-pair RoPE of every Q_i and K_i (apply_rotary_emb,
+ * Ndiff_transformer.py:11-22 / control.py:11-22, rotation in fp32 then cast).
+ * inverse != 0 applies the conjugate rotation (its backward).
+ * src may be fp32 (src_f32 != 0) or dtype; dst is dtype.
+ * freqs: fp32 [T][head_size/2][2] = view_as_real(freqs_cis[:T]). */
+typedef struct dta_rope_args {
+  int32_t dtype;
+  int32_t B, T, H, n_terms, head_size;
+  int32_t inverse, src_f32;
+  dta_tensor src, dst;               /* [b][t][h][i][d] */
+  const float* freqs;
+} dta_rope_args;
+
+int dta_rope(const dta_rope_args* a, void* stream);
+
+/* Cast/copy a [b][t][h][i][d] tensor from fp32 to dtype (dQ finalisation). */
+int dta_cast_f32(int32_t dtype, int32_t B, int32_t T, int32_t H, int32_t n_terms,
+                 int32_t head_size, const float* src, dta_tensor dst, void* stream);
+
+const char* dta_error_string(int code);
+int dta_abi_version(void);
+/* 1 if (dtype, head_size, n_terms, dv) has compiled kernels. */
+int dta_supported(int32_t dtype, int32_t head_size, int32_t n_terms, int32_t dv);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DIFFATTN_H_ */

@@ -1,0 +1,141 @@
+"""GPU parity: the HIP kernels (through the C ABI) against the CPU oracle.
+
+Tolerance (SURVEY section 4 norm, max|a-b|/max|b| per tensor; BASELINE.json
+north_star): fp32 <= 1e-4, bf16/fp16 <= 2e-2, on outputs and every gradient.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import Golden, rel_err
+from oracle import diffattn_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+TOL = {torch.float32: 1e-4, torch.bfloat16: 2e-2, torch.float16: 2e-2}
+DEV = "cuda"
+
+
+def _ops():
+    from differential_transformer_replication_amd import ops
+    return ops
+
+
+def _oracle_core(qkv64, coef64, H, N, hs, freqs_c=None):
+    """Per-head oracle on the packed layout (CPU fp64)."""
+    B, T, W = qkv64.shape
+    dv = 2 * hs
+    nq = H * N * hs
+    q = qkv64[..., :nq].view(B, T, H, N, hs)
+    k = qkv64[..., nq:2 * nq].view(B, T, H, N, hs)
+    v = qkv64[..., 2 * nq:].view(B, T, H, dv)
+    outs = []
+    for h in range(H):
+        qs = [q[:, :, h, i] for i in range(N)]
+        ks = [k[:, :, h, i] for i in range(N)]
+        if freqs_c is not None:
+            qs = [_rope64(t, freqs_c) for t in qs]
+            ks = [_rope64(t, freqs_c) for t in ks]
+        outs.append(orc.diff_core(qs, ks, v[:, :, h], coef64[h]))
+    return torch.cat(outs, dim=-1)
+
+
+def _rope64(x, freqs_c):
+    # fp64 restatement of apply_rotary_emb (the oracle's own is fp32 by definition)
+    T = x.shape[1]
+    ang = torch.view_as_real(freqs_c[:T]).double()
+    c, s = ang[..., 0], ang[..., 1]
+    a, b = x[..., 0::2], x[..., 1::2]
+    out = torch.stack([a * c - b * s, a * s + b * c], dim=-1)
+    return out.flatten(-2)
+
+
+CASES = [  # H, N, hs, T, rope
+    (2, 2, 64, 129, False), (1, 2, 16, 7, False), (3, 2, 32, 200, False), (2, 3, 64, 65, True),
+    (2, 4, 32, 97, True), (1, 1, 64, 64, True), (2, 2, 128, 130, False), (1, 4, 64, 70, False),
+    (2, 2, 64, 1, False), (1, 2, 64, 256, True),
+]
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("H,N,hs,T,rope", CASES)
+def test_core_fwd_bwd(dtype, H, N, hs, T, rope):
+    ops = _ops()
+    from differential_transformer_replication_amd import _lib
+    if not _lib.supported(dtype, hs, N, 2 * hs):
+        pytest.skip("configuration not built")
+    g = torch.Generator().manual_seed(1000 * H + 100 * N + hs + T)
+    B = 2
+    W = ops.packed_width(H, N, hs, 2 * hs)
+    qkv = torch.randn(B, T, W, generator=g)
+    coef = torch.randn(H, N, generator=g) * 0.5
+    coef[:, 0] = 1.0
+    do = torch.randn(B, T, H * 2 * hs, generator=g)
+    freqs_c = orc.precompute_freqs_cis(hs, max(T, 8)) if rope else None
+    # quantise inputs to the kernel dtype so both sides see identical values
+    qkv_q = qkv.to(dtype).double()
+    do_q = do.to(dtype).double()
+    x64 = qkv_q.clone().requires_grad_(True)
+    c64 = coef.double().clone().requires_grad_(True)
+    ref = _oracle_core(x64, c64, H, N, hs, freqs_c)
+    ref.backward(do_q)
+
+    xg = qkv.to(dtype).to(DEV).requires_grad_(True)
+    cg = coef.to(DEV).requires_grad_(True)
+    freqs = torch.view_as_real(freqs_c[:T]).contiguous().to(DEV) if rope else None
+    out = ops.diff_attention(xg, cg, H, N, hs, freqs)
+    out.backward(do.to(dtype).to(DEV))
+    torch.cuda.synchronize()
+    tol = TOL[dtype]
+    assert rel_err(out.float().cpu(), ref) < tol
+    nq = H * N * hs
+    gx = xg.grad.float().cpu()
+    assert rel_err(gx[..., :nq], x64.grad[..., :nq]) < tol, "dQ"
+    assert rel_err(gx[..., nq:2 * nq], x64.grad[..., nq:2 * nq]) < tol, "dK"
+    assert rel_err(gx[..., 2 * nq:], x64.grad[..., 2 * nq:]) < tol, "dV"
+    assert rel_err(cg.grad.cpu(), c64.grad) < tol, "dcoef"
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("C", [48, 384, 2048, 4104])
+def test_group_ln_scale(dtype, C):
+    ops = _ops()
+    g = torch.Generator().manual_seed(C)
+    x = torch.randn(3, 37, C, generator=g) * 3 + 1
+    w = 1 + 0.1 * torch.randn(1, 1, C, generator=g)
+    b = 0.1 * torch.randn(1, 1, C, generator=g)
+    dy = torch.randn(3, 37, C, generator=g)
+    xq = x.to(dtype).double().requires_grad_(True)
+    w64 = w.double().requires_grad_(True)
+    b64 = b.double().requires_grad_(True)
+    ref = orc.group_layer_norm(xq, w64, b64) * (1 - torch.tensor(0.8).double())
+    ref.backward(dy.to(dtype).double())
+    xg = x.to(dtype).to(DEV).requires_grad_(True)
+    wg = w.to(DEV).requires_grad_(True)
+    bg = b.to(DEV).requires_grad_(True)
+    out = ops.group_ln_scale(xg, wg, bg, 1e-5, float(1 - torch.tensor(0.8)))
+    out.backward(dy.to(dtype).to(DEV))
+    tol = TOL[dtype]
+    assert rel_err(out.float().cpu(), ref) < tol
+    assert rel_err(xg.grad.float().cpu(), xq.grad) < tol
+    assert rel_err(wg.grad.cpu(), w64.grad) < tol
+    assert rel_err(bg.grad.cpu(), b64.grad) < tol
+
+
+def test_rope_kernel_matches_reference_fixture(golden):
+    """dta_rope (fp32) bitwise-close to the reference apply_rotary_emb fixture."""
+    from differential_transformer_replication_amd import _lib
+    lib = _lib.load()
+    fc = torch.view_as_complex(torch.from_numpy(golden["rope/freqs"]).contiguous())
+    x = torch.from_numpy(golden["rope/x"])                      # (2, 17, 32)
+    want = torch.from_numpy(golden["rope/out"])
+    B, T, hs = x.shape
+    src = x.view(B, T, 1, 1, hs).to(DEV)
+    dst = torch.empty_like(src)
+    freqs = torch.view_as_real(fc[:T]).contiguous().to(DEV)
+    a = _lib.RopeArgs(_lib.DTA_F32, B, T, 1, 1, hs, 0, 0, _lib.tensor5(src), _lib.tensor5(dst), freqs.data_ptr())
+    _lib.check(lib.dta_rope(a, _lib.stream_handle(src.device)))
+    torch.cuda.synchronize()
+    assert (dst.view(B, T, hs).cpu() - want).abs().max().item() < 1e-6
