@@ -1,0 +1,190 @@
+#!/usr/bin/env python
+"""Benchmark of the differential-attention hot path on MI355X.
+
+Default (``--mode kernel``): BASELINE.json configs[1] -- the fused N=2
+differential-attention core, bf16, B=8 per GPU, H=16, head_size=64, dv=128,
+T=4096, causal, forward + backward, on synthetic N(0,1) inputs resident in HBM.
+One step = one forward + one backward of that core over one batch.  With N
+GPUs (torchrun, one process per GPU over RCCL) every rank runs its own batch
+shard: the path shards by batch with no data-path collective ("weak" scaling);
+only the timing uses a barrier and a MAX all-reduce.
+
+``value`` = algorithmic TFLOP/s of the whole job: ranks x 3*F_fwd per step /
+step time, F_fwd = B*H*T^2*(N*hs + dv) (causal-halved matmul FLOPs).
+``roofline`` reports the dominant kernel (the fused backward) from HIP events
+bracketing its launches inside the timed region.  ``cpu_baseline`` times the CPU
+oracle (the reference's algorithm op for op: per-head loop, materialised T x T
+maps, fp32) on a bounded sample on this host.
+
+``--mode train``: data-parallel training tokens/s of a reference-architecture
+model (see differential_transformer_replication_amd/train.py).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "diff-attn fwd+bwd TFLOP/s (% MFMA peak); train tokens/sec at 1/2/4/8 GPUs"
+PEAK_BF16_TFLOPS = 2516.6          # 256 CU x 2.4 GHz x 4096 flop/clk/CU (dense, MI355X_MICROARCH.md)
+
+
+def _dist():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    return world, rank, local
+
+
+def _sync(world):
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+        torch.cuda.synchronize()
+
+
+def _max_over_ranks(x: float, world: int) -> float:
+    if world == 1:
+        return x
+    t = torch.tensor([x], device="cuda", dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def cpu_baseline(T=4096, H=16, hs=64, reps=2):
+    """Oracle (reference algorithm, eager fp32, per-head loop) on the host CPU.
+    Bounded sample: B=1, H=16 at the full T; heads and batch entries are
+    independent so the rate per FLOP carries to B=8."""
+    from oracle import diffattn_oracle as orc
+    threads = max(1, min(16, os.cpu_count() or 1))
+    torch.set_num_threads(threads)
+    g = torch.Generator().manual_seed(0)
+    dv = 2 * hs
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        for _h in range(H):
+            q = [torch.randn(1, T, hs, generator=g, requires_grad=True) for _ in range(2)]
+            k = [torch.randn(1, T, hs, generator=g, requires_grad=True) for _ in range(2)]
+            v = torch.randn(1, T, dv, generator=g, requires_grad=True)
+            lam = torch.tensor(0.47, requires_grad=True)
+            coef = torch.stack([torch.ones(()), -lam])
+            out = orc.diff_core(q, k, v, coef)
+            out.backward(torch.randn(1, T, dv, generator=g))
+        ts.append(time.perf_counter() - t0)
+    f_fwd, f_bwd = orc.flops_attention(1, H, T, hs, dv, 2)
+    sec = sum(ts) / len(ts)
+    return {"value": round((f_fwd + f_bwd) / sec / 1e12, 6), "unit": "TFLOP/s", "cores": threads,
+            "kind": "port",
+            "sample": f"CPU oracle (reference algorithm op for op, eager fp32, per-head loop, materialised "
+                      f"T x T maps) fwd+bwd of B=1 H={H} T={T} hs={hs} N=2, mean of {reps}; "
+                      f"{sec:.2f} s per sample; rate per algorithmic FLOP, same FLOP count as the GPU step"}
+
+
+def kernel_bench(args, world, rank):
+    from differential_transformer_replication_amd import ops
+    from differential_transformer_replication_amd.diff_transformer import _layer_lambda_coef
+    from differential_transformer_replication_amd._compat import lambda_init_value
+    B, H, hs, N, T = args.batch, 16, 64, 2, args.seq
+    dv = 2 * hs
+    dev = torch.device("cuda", torch.cuda.current_device())
+    W = ops.packed_width(H, N, hs, dv)
+    g = torch.Generator(device=dev).manual_seed(0 + rank)
+    qkv = torch.randn(B, T, W, device=dev, dtype=torch.bfloat16, generator=g).requires_grad_(True)
+    do = torch.randn(B, T, H * dv, device=dev, dtype=torch.bfloat16, generator=g)
+    g1 = torch.Generator(device=dev).manual_seed(1)
+    lam = [torch.randn(H, hs, device=dev, generator=g1) * 0.1 for _ in range(4)]
+    coef = _layer_lambda_coef(*lam, lambda_init_value(3, None))
+
+    def step():
+        qkv.grad = None
+        out = ops.diff_attention(qkv, coef, H, N, hs)
+        out.backward(do)
+
+    for _ in range(args.warmup):
+        step()
+    _sync(world)
+    ops.TIMER.start()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    _sync(world)
+    el = time.perf_counter() - t0
+    ops.TIMER.stop()
+    el = _max_over_ranks(el, world)
+    kt = ops.TIMER.mean_ms()
+    f_fwd = float(B) * H * T * T * (N * hs + dv)
+    f_bwd = 2 * f_fwd
+    ms = el / args.steps * 1e3
+    value = world * (f_fwd + f_bwd) / (el / args.steps) / 1e12
+    t_fwd, n_fwd = kt["attn_fwd"]
+    t_bwd, n_bwd = kt["attn_bwd"]
+    # algorithmic HBM bytes: fwd reads Q_i, K_i, V and writes O (+ the O_i the bwd needs)
+    kernels = {
+        "attn_fwd": {"ms": round(t_fwd, 4), "launches": n_fwd, "tflops": round(f_fwd / t_fwd / 1e9, 2)},
+        "attn_bwd": {"ms": round(t_bwd, 4), "launches": n_bwd, "tflops": round(f_bwd / t_bwd / 1e9, 2)},
+    }
+    dom = "attn_bwd" if t_bwd >= t_fwd else "attn_fwd"
+    achieved = kernels[dom]["tflops"]
+    res = {
+        "metric": METRIC, "value": round(value, 3), "unit": "TFLOP/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
+        "config": {"workload": "cfg2: fused N=2 diff-attention core fwd+bwd (BASELINE configs[1])",
+                   "batch_per_gpu": B, "global_batch": B * world, "heads": H, "head_size": hs, "dv": dv,
+                   "seq_len": T, "n_terms": N, "causal": True,
+                   "parallelism": f"batch-sharded replicas x{world} (no data-path collective)"},
+        "mfma_frac_step": round(value / world / PEAK_BF16_TFLOPS, 4),
+        "kernels": kernels,
+        "roofline": {"bound": "mfma", "kernel": dom, "achieved": achieved, "peak": PEAK_BF16_TFLOPS,
+                     "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
+                     "traffic": args.traffic},
+    }
+    return res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--mode", choices=["kernel", "train"], default="kernel")
+    ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--seq", type=int, default=4096)
+    ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
+    ap.add_argument("--traffic", type=float, default=None,
+                    help="HBM bytes per dominant-kernel launch from rocprofv3 PMC (profiles/)")
+    args = ap.parse_args()
+    world, rank, local = _dist()
+    if args.mode == "kernel":
+        res = kernel_bench(args, world, rank)
+    else:
+        from differential_transformer_replication_amd.train import train_bench
+        res = train_bench(args, world, rank)
+    if rank == 0:
+        if args.cpu_baseline == "auto" and world == 1:
+            res["cpu_baseline"] = cpu_baseline()
+        else:
+            res["cpu_baseline"] = None
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -46,7 +46,11 @@ class AttnBwdArgs(ctypes.Structure):
                 ("q", DtaTensor), ("k", DtaTensor), ("v", DtaTensor), ("obr", DtaTensor),
                 ("lse", ctypes.c_void_p), ("coef", ctypes.c_void_p), ("dout", DtaTensor),
                 ("dq", DtaTensor), ("dk", DtaTensor), ("dv_out", DtaTensor),
-                ("dcoef", ctypes.c_void_p), ("delta", ctypes.c_void_p), ("dq_f32", ctypes.c_void_p)]
+                ("dcoef", ctypes.c_void_p), ("delta", ctypes.c_void_p), ("dq_f32", ctypes.c_void_p),
+                ("stages", ctypes.c_int32)]
+
+
+BWD_PRE, BWD_MAIN, BWD_POST = 1, 2, 4
 
 
 class LnArgs(ctypes.Structure):

@@ -137,13 +137,18 @@ int dta_attn_bwd(const dta_attn_bwd_args* a, void* stream) {
     return DTA_ERR_INVALID;
   if (a->dq.ptr && !ok_tensor(a->dq, a->dtype, true)) return DTA_ERR_INVALID;
   const int B = a->B, T = a->T, H = a->H, N = a->n_terms, HS = a->head_size;
-  int e = (int)hipMemsetAsync(a->dq_f32, 0, (size_t)B * T * H * N * HS * 4, st);
-  if (e) return DTA_ERR_LAUNCH;
-  DeltaParams dp{};
-  dp.dout = t5(a->dout); dp.obr = t5(a->obr); dp.delta = a->delta;
-  dp.B = B; dp.T = T; dp.H = H; dp.N = N; dp.DV = a->dv;
-  if ((e = launch_delta(a->dtype, dp, st))) return status(e);
-  if ((e = launch_dcoef(a->delta, a->dcoef, B, T, H, N, st))) return status(e);
+  const int stages = a->stages ? a->stages : (DTA_BWD_PRE | DTA_BWD_MAIN | DTA_BWD_POST);
+  int e = 0;
+  if (stages & DTA_BWD_PRE) {
+    if (hipMemsetAsync(a->dq_f32, 0, (size_t)B * T * H * N * HS * 4, st)) return DTA_ERR_LAUNCH;
+    DeltaParams dp{};
+    dp.dout = t5(a->dout); dp.obr = t5(a->obr); dp.delta = a->delta;
+    dp.B = B; dp.T = T; dp.H = H; dp.N = N; dp.DV = a->dv;
+    if ((e = launch_delta(a->dtype, dp, st))) return status(e);
+    if ((e = launch_dcoef(a->delta, a->dcoef, B, T, H, N, st))) return status(e);
+  }
+  if (!(stages & DTA_BWD_MAIN)) goto post;
+  {
   BwdParams p{};
   p.q = t5(a->q); p.k = t5(a->k); p.v = t5(a->v); p.dout = t5(a->dout);
   p.dk = t5(a->dk); p.dv = t5(a->dv_out);
@@ -151,7 +156,9 @@ int dta_attn_bwd(const dta_attn_bwd_args* a, void* stream) {
   p.B = B; p.T = T; p.H = H; p.N = N; p.HS = HS; p.DV = a->dv;
   p.scale = a->scale; p.sl2 = a->scale * kLog2e;
   if ((e = launch_attn_bwd(a->dtype, p, st))) return status(e);
-  if (a->dq.ptr) {
+  }
+post:
+  if ((stages & DTA_BWD_POST) && a->dq.ptr) {
     if ((e = launch_cast(a->dtype, a->dq_f32, t5(a->dq), B, T, H, N, HS, st))) return status(e);
   }
   return DTA_OK;

@@ -15,8 +15,9 @@ There is no CPU or eager fallback: non-CUDA tensors raise.
 """
 from __future__ import annotations
 
+import contextlib
 import math
-from typing import Optional
+from typing import Dict, List, Optional, Tuple
 
 import torch
 
@@ -30,6 +31,42 @@ def _require_gpu(*ts: Tensor) -> None:
         if t is not None and t.device.type != "cuda":
             raise RuntimeError("differential_transformer_replication_amd ops run only on the MI355X "
                                "HIP path (libdiffattn.so); got a tensor on " + str(t.device))
+
+
+class KernelTimer:
+    """Optional HIP-event brackets around the two dominant launches (the fused
+    forward kernel and the fused backward kernel).  Events are recorded on the
+    stream the kernels are launched on (torch's current stream), so each pair
+    brackets exactly one kernel.  Off by default (no events, no overhead)."""
+
+    def __init__(self):
+        self.active = False
+        self._pairs: Dict[str, List[Tuple[torch.cuda.Event, torch.cuda.Event]]] = {}
+
+    def start(self):
+        self._pairs = {}
+        self.active = True
+
+    def stop(self):
+        self.active = False
+
+    @contextlib.contextmanager
+    def region(self, name: str):
+        if not self.active:
+            yield
+            return
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        yield
+        e1.record()
+        self._pairs.setdefault(name, []).append((e0, e1))
+
+    def mean_ms(self) -> Dict[str, Tuple[float, int]]:
+        torch.cuda.synchronize()
+        return {k: (sum(a.elapsed_time(b) for a, b in v) / len(v), len(v)) for k, v in self._pairs.items()}
+
+
+TIMER = KernelTimer()
 
 
 def packed_width(H: int, N: int, hs: int, dv: int) -> int:
@@ -81,7 +118,8 @@ class _DiffAttention(torch.autograd.Function):
         a = _lib.AttnFwdArgs(dt, B, T, H, N, hs, dv, 1.0 / math.sqrt(hs), 0.0,
                              _lib.tensor5(q), _lib.tensor5(k), _lib.tensor5(v), _lib.tensor5(o), obr_t,
                              lse.data_ptr(), coef.data_ptr())
-        _lib.check(lib.dta_attn_fwd(a, stream))
+        with TIMER.region("attn_fwd"):
+            _lib.check(lib.dta_attn_fwd(a, stream))
         ctx.save_for_backward(qkv, qk_rot, obr, lse, coef, freqs)
         ctx.dims = (H, N, hs, dv)
         return o.view(B, T, H * dv)
@@ -113,7 +151,12 @@ class _DiffAttention(torch.autograd.Function):
                              lse.data_ptr(), coef.data_ptr(), _lib.tensor5(do),
                              null if rope else _lib.tensor5(dq),
                              _lib.tensor5(dk_rot if rope else dk), _lib.tensor5(dvv),
-                             dcoef.data_ptr(), delta.data_ptr(), dq32.data_ptr())
+                             dcoef.data_ptr(), delta.data_ptr(), dq32.data_ptr(), _lib.BWD_PRE)
+        _lib.check(lib.dta_attn_bwd(a, stream))
+        a.stages = _lib.BWD_MAIN
+        with TIMER.region("attn_bwd"):
+            _lib.check(lib.dta_attn_bwd(a, stream))
+        a.stages = _lib.BWD_POST
         _lib.check(lib.dta_attn_bwd(a, stream))
         if rope:
             # gradients back through the rotation: conjugate rotate (Ndiff_transformer.py:11-22 bwd)

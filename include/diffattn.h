@@ -98,7 +98,13 @@ typedef struct dta_attn_bwd_args {
   float* dcoef;              /* output fp32 [h][i] (overwritten) */
   float* delta;              /* workspace fp32 [i][b][h][t] */
   float* dq_f32;             /* workspace fp32 [b][t][h][i][d] */
+  int32_t stages;            /* 0 = all; else bitmask of DTA_BWD_PRE (zero dq_f32,
+                                delta, dcoef), DTA_BWD_MAIN (the fused kernel),
+                                DTA_BWD_POST (dq cast) -- lets a caller bracket
+                                one stage with events on the same stream */
 } dta_attn_bwd_args;
+
+enum { DTA_BWD_PRE = 1, DTA_BWD_MAIN = 2, DTA_BWD_POST = 4 };
 
 int dta_attn_bwd(const dta_attn_bwd_args* a, void* stream);
 size_t dta_attn_bwd_workspace_bytes(int32_t B, int32_t T, int32_t H, int32_t n_terms,
