@@ -50,7 +50,7 @@ class AttnBwdArgs(ctypes.Structure):
                 ("stages", ctypes.c_int32)]
 
 
-BWD_PRE, BWD_MAIN, BWD_POST = 1, 2, 4
+BWD_PRE, BWD_DQ, BWD_DKDV = 1, 2, 4
 
 
 class LnArgs(ctypes.Structure):

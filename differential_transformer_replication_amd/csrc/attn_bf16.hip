@@ -3,6 +3,7 @@
 
 namespace dta {
 int launch_attn_fwd_bf16(const FwdParams& p, hipStream_t st) { return dispatch_fwd<__bf16>(p, st); }
-int launch_attn_bwd_bf16(const BwdParams& p, hipStream_t st) { return dispatch_bwd<__bf16>(p, st); }
+int launch_attn_dq_bf16(const BwdParams& p, hipStream_t st) { return dispatch_dq<__bf16>(p, st); }
+int launch_attn_dkdv_bf16(const BwdParams& p, hipStream_t st) { return dispatch_dkdv<__bf16>(p, st); }
 bool attn_supported_bf16(int hs, int n) { return supported_t<__bf16>(hs, n); }
 }  // namespace dta

@@ -3,6 +3,7 @@
 
 namespace dta {
 int launch_attn_fwd_f16(const FwdParams& p, hipStream_t st) { return dispatch_fwd<_Float16>(p, st); }
-int launch_attn_bwd_f16(const BwdParams& p, hipStream_t st) { return dispatch_bwd<_Float16>(p, st); }
+int launch_attn_dq_f16(const BwdParams& p, hipStream_t st) { return dispatch_dq<_Float16>(p, st); }
+int launch_attn_dkdv_f16(const BwdParams& p, hipStream_t st) { return dispatch_dkdv<_Float16>(p, st); }
 bool attn_supported_f16(int hs, int n) { return supported_t<_Float16>(hs, n); }
 }  // namespace dta

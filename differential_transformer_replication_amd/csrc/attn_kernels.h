@@ -1,33 +1,141 @@
 // attn_kernels.h -- fused N-branch causal differential attention, gfx950.
 //
-// Forward (replaces diff_transformer.py:57-72 for every head at once, and the
-// branch loop of Ndiff_transformer.py:102-125):
-//   O = sum_i c[h][i] * softmax_causal(Q_i K_i^T * scale) V
-// One workgroup = 4 waves = 128 query rows of one (b, h, dv-chunk); each wave
-// owns 32 rows.  Key tiles of BN rows of every K_i and of V are staged in LDS
-// once per workgroup and feed all N branches.  Scores are computed transposed
-// (S^T = K Q^T, key in registers, query on the lane), so the online softmax of
-// a query row lives in one lane pair (l, l^32) and P^T is already the B
-// operand of O^T += V^T P^T (V^T read from the row-major V tile with
-// ds_read_b64_tr_b16).  Outputs: the combined O, the per-branch normalised
-// O_i (for the backward's delta_i) and the per-branch log2-sum-exp.
+//   O = sum_i c[h][i] * softmax_causal(Q_i K_i^T * scale) V        (all heads)
 //
-// Backward: one workgroup = NW waves = NW*32 keys of one (b, h); each wave
-// keeps dK_i^T and dV^T of its 32 keys in registers while the workgroup sweeps
-// 32-row query tiles at and below the diagonal.  S is computed with the key on
-// the lane, so P, dS are directly the B operands of dV^T += dO^T P_c and
-// dK_i^T += Q_i^T dS_i; dS crosses LDS once for dQ_i = dS_i K_i, which is
-// summed across key blocks with fp32 atomics.  dS_i = c_i P_i (dP - delta_i),
-// dP = dO V^T shared by all branches, P_c = sum_i c_i P_i.
+// Replaces DiffHead/MultiHeadDiffAttention's per-head eager loop
+// (diff_transformer.py:57-72, 89) and AlternatingDiffHead's branch loop
+// (Ndiff_transformer.py:102-125).  Three kernels, all flash-style loops whose
+// tiles arrive in LDS by LDS-DMA (global_load_lds, one 1 KiB piece per wave
+// instruction) into double buffers, so the next tile streams in while MFMAs
+// consume the current one:
+//
+//  attn_fwd   query-major.  Workgroup = NW waves x 32 query rows of one
+//             (b, h, dv-chunk).  Scores transposed (S^T = K Q^T: key in
+//             registers, query on the lane) so each query row's online
+//             softmax lives in one lane pair and P^T is directly the B operand
+//             of O^T += V^T P^T.  V^T comes from the row-major V tile through
+//             ds_read_b64_tr_b16.  Writes O, the per-branch normalised O_i and
+//             the per-branch log2-sum-exp.
+//  attn_dq    query-major backward for dQ (no atomics):
+//             S^T_i = K_i Q_i^T, dP^T = V dO^T, dS^T_i = c_i P^T_i (dP^T - delta_i),
+//             dQ_i^T += K_i^T dS^T_i.  Also computes delta_i = <dO, O_i> per row
+//             (written for attn_dkdv) and d(coef) = sum delta_i.
+//  attn_dkdv  key-major backward: S_i = Q_i K_i^T, dP = dO V^T (key on the lane),
+//             dK_i^T += Q_i^T dS_i, dV^T += dO^T (sum_i c_i P_i).
+//
+// LDS images are rows of 16-byte chunks with an XOR swizzle (swz<ROWB>) that
+// makes both access kinds conflict-free: 32-distinct-row ds_read_b128 operand
+// reads and 4-row x 32-column ds_read_b64_tr_b16 transposed reads.  LDS-DMA
+// writes lane-linearly, so the swizzle is applied to the per-lane SOURCE
+// address and to every read (cdna_hip_programming.md rule 21).
 #pragma once
 #include "dta_common.h"
 #include "dta_internal.h"
 
 namespace dta {
 
-constexpr int FWD_WAVES = 4;
-constexpr int FWD_BM = FWD_WAVES * 32;
+// ------------------------------------------------------------ LDS images ---
+template <int ROWB>
+__device__ __forceinline__ int swz(int r) {
+  if constexpr (ROWB >= 256) return ((r & 3) << 2) | ((r >> 2) & 3);
+  else if constexpr (ROWB == 128) return (((r >> 1) & 1) << 2) | ((r >> 2) & 3);
+  else if constexpr (ROWB == 64) return (r >> 2) & 3;
+  else return (r >> 3) & 1;
+}
 
+template <class E, int COLS>
+struct Img {
+  static constexpr int ES = (int)sizeof(E);
+  static constexpr int ROWB = COLS * ES;
+  static constexpr int CPR = ROWB / 16;
+  static_assert(ROWB >= 32 && (ROWB & (ROWB - 1)) == 0, "image rows must be a power of two >= 32 B");
+  __device__ static int off(int r, int col) {   // element offset of (r, col)
+    const int byte = col * ES;
+    return (r * ROWB + ((((byte >> 4) ^ swz<ROWB>(r)) << 4) | (byte & 15))) / ES;
+  }
+  using O = Ops<E>;
+  using frag = typename O::frag;
+  // operand fragment of k-step s: row r, k = s*KSTEP + h*KH (+0..KH-1)
+  __device__ static frag row(const E* img, int r, int s, int h) {
+    if constexpr (ES == 2) return *reinterpret_cast<const frag*>(img + off(r, s * 16 + h * 8));
+    else return img[off(r, 2 * s + h)];
+  }
+  // 4 rows r0..r0+3 x 16 columns per 16-lane group (ds_read_b64_tr_b16)
+  template <class V4>
+  __device__ static V4 tr4(const E* img, int r0, int cbase, int lane) {
+    const int i = lane & 15;
+    const E* p = img + off(r0 + (i >> 2), cbase + ((lane >> 4) & 1) * 16 + (i & 3) * 4);
+    s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p));
+    return __builtin_bit_cast(V4, v);
+  }
+  // transposed operand, k order matching an accumulator packed by pack<s>():
+  // element j <-> row rbase + 16s + 8(j>>2) + 4h + (j&3), column cbase + (lane&31)
+  __device__ static frag tr_perm(const E* img, int rbase, int s, int h, int cbase, int lane) {
+    if constexpr (ES == 2) {
+      typedef E v4 __attribute__((ext_vector_type(4)));
+      v4 lo = tr4<v4>(img, rbase + 16 * s + 4 * h, cbase, lane);
+      v4 hi = tr4<v4>(img, rbase + 16 * s + 8 + 4 * h, cbase, lane);
+      return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    } else {
+      return img[off(rbase + (s & 3) + 8 * (s >> 2) + 4 * h, cbase + (lane & 31))];
+    }
+  }
+};
+
+// Stage ROWS x COLS elements (rows row0.., clamped to rowmax; only the first
+// VALID columns come from memory) into an image.  Whole-row 1 KiB pieces go by
+// LDS-DMA; images with padded columns are staged through registers (zero-fill).
+template <class E, int COLS, int ROWS, int VALID, int NTHR>
+__device__ __forceinline__ void stage(E* img, const E* g, int64_t rs, int row0, int rowmax, int tid) {
+  using I = Img<E, COLS>;
+  constexpr int BYTES = ROWS * I::ROWB;
+  if constexpr (VALID == COLS && BYTES % 1024 == 0) {
+    constexpr int NI = BYTES / 1024;
+    const int wave = tid >> 6, lane = tid & 63;
+#pragma unroll
+    for (int j0 = 0; j0 < NI; j0 += NTHR / 64) {
+      const int j = j0 + wave;
+      if (NI % (NTHR / 64) == 0 || j < NI) {
+        const int pb = j * 1024 + lane * 16;
+        const int r = pb / I::ROWB;
+        const int c = ((pb % I::ROWB) >> 4) ^ swz<I::ROWB>(r);
+        const int row = min(row0 + r, rowmax);
+        const char* src = reinterpret_cast<const char*>(g + (int64_t)row * rs) + c * 16;
+        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(reinterpret_cast<char*>(img) + j * 1024),
+                                         16, 0, 0);
+      }
+    }
+  } else {
+    constexpr int CH = ROWS * I::CPR;
+    for (int c = tid; c < CH; c += NTHR) {
+      const int r = c / I::CPR, ch = c % I::CPR;
+      const int row = row0 + r;
+      const bool ok = row <= rowmax && ch * 16 < VALID * I::ES;
+      s16x8 v = ok ? *reinterpret_cast<const s16x8*>(reinterpret_cast<const char*>(g + (int64_t)row * rs) + ch * 16)
+                   : s16x8{};
+      *reinterpret_cast<s16x8*>(reinterpret_cast<char*>(img) + r * I::ROWB + ((ch ^ swz<I::ROWB>(r)) << 4)) = v;
+    }
+  }
+}
+
+// Per-row fp32 vectors (LSE / delta) of NR rows x N branches by 4-byte LDS-DMA.
+// src layout [i][b][h][t]: branch stride bs; dst [i][NR] (padded to 64-float pieces).
+template <int N, int NR, int NTHR>
+__device__ __forceinline__ void stage_rows(float* dst, const float* src, int64_t bs, int row0, int rowmax, int tid) {
+  constexpr int TOT = N * NR;
+  constexpr int NI = (TOT + 63) / 64;
+  const int wave = tid >> 6, lane = tid & 63;
+  for (int j = wave; j < NI; j += NTHR / 64) {
+    const int e = j * 64 + lane;
+    const int i = min(e / NR, N - 1), r = e % NR;
+    const float* s = src + i * bs + min(row0 + r, rowmax);
+    __builtin_amdgcn_global_load_lds(s, (__attribute__((address_space(3))) void*)(dst + j * 64), 4, 0, 0);
+  }
+}
+
+__device__ __forceinline__ void wait_dma() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// ---------------------------------------------------------------- forward ---
 template <class E> struct FwdTile { static constexpr int BN = 64; };
 template <> struct FwdTile<float> { static constexpr int BN = 32; };
 
@@ -38,41 +146,60 @@ struct FwdChunk {
   static constexpr int DVC = DV <= cap ? DV : (cap >= 128 && DV % 128 == 0 ? 128 : (cap >= 64 ? 64 : 32));
 };
 
-template <class E, int HS, int N, int DVC>
-struct FwdSmem {
+template <class E, int HS, int N, int DVC, int NW, bool QREG>
+struct FwdCfg {
   static constexpr int BN = FwdTile<E>::BN;
-  static constexpr int KSTR = HS + Pad<E>::v;
-  static constexpr int VSTR = DVC + (sizeof(E) == 2 ? 32 : 0);
-  static constexpr int bytes = (N * BN * KSTR + BN * VSTR) * (int)sizeof(E);
+  static constexpr int BM = NW * 32;
+  static constexpr int nQ = QREG ? 0 : N * BM * HS;
+  static constexpr int nK = N * BN * HS;
+  static constexpr int nV = BN * DVC;
+  static constexpr int bytes = (nQ + 2 * nK + 2 * nV) * (int)sizeof(E);
 };
 
-template <class E, int HS, int N, int DVC>
-__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(FwdParams p) {
+template <class E, int HS, int N>
+struct FwdPick {
+  static constexpr int DVC = FwdChunk<N, 2 * HS>::DVC;
+  static constexpr int LIM = 160 * 1024;
+  static constexpr int NWMAX = sizeof(E) == 2 ? 8 : 4;
+  // widest workgroup with Q in LDS, else Q in registers
+  static constexpr bool q8 = NWMAX >= 8 && FwdCfg<E, HS, N, DVC, 8, false>::bytes <= LIM;
+  static constexpr bool q4 = FwdCfg<E, HS, N, DVC, 4, false>::bytes <= LIM;
+  static constexpr int NW = q8 ? 8 : (q4 ? 4 : 4);
+  static constexpr bool QREG = !(q8 || q4);
+  static constexpr bool ok = FwdCfg<E, HS, N, DVC, NW, QREG>::bytes <= LIM;
+};
+
+template <class E, int HS, int N, int DVC, int NW, bool QREG>
+__global__ __launch_bounds__(NW * 64, 2) void attn_fwd_kernel(FwdParams p) {
   using O = Ops<E>;
   using frag = typename O::frag;
-  constexpr int BN = FwdTile<E>::BN;
+  using QI = Img<E, HS>;
+  using KI = Img<E, HS>;
+  using VI = Img<E, DVC>;
+  using CF = FwdCfg<E, HS, N, DVC, NW, QREG>;
+  constexpr int BN = CF::BN, BM = CF::BM, NTHR = NW * 64;
   constexpr int KS = O::KSTEP;
-  constexpr int KSTR = FwdSmem<E, HS, N, DVC>::KSTR;
-  constexpr int VSTR = FwdSmem<E, HS, N, DVC>::VSTR;
-  constexpr int NSQ = HS / KS;          // k-steps of QK^T
-  constexpr int NKB = BN / 32;          // 32-key blocks per tile
-  constexpr int SPB = 32 / KS;          // PV k-steps per 32-key block
+  constexpr int NSQ = HS / KS;
+  constexpr int NKB = BN / 32;
+  constexpr int SPB = 32 / KS;
   constexpr int NDB = DVC / 32;
-  constexpr int VEC = O::VEC;
+  constexpr float THR = 8.f;        // deferred-rescale threshold (log2 units): P <= 2^8
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  E* Ks = reinterpret_cast<E*>(smem);
-  E* Vs = Ks + N * BN * KSTR;
+  E* Qs = reinterpret_cast<E*>(smem);
+  E* Kb = Qs + CF::nQ;              // [2][N][BN][HS]
+  E* Vb = Kb + 2 * CF::nK;          // [2][BN][DVC]
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int hf = lane >> 5, c32 = lane & 31;
+  const int wave = threadIdx.x >> 6;
+  int tid = threadIdx.x, lane = tid & 63;
+  int hf = lane >> 5, c32 = lane & 31;
   const int nch = p.DV / DVC;
-  const int qt = gridDim.x - 1 - blockIdx.x;           // longest (causal) tiles first
+  const int qt = gridDim.x - 1 - blockIdx.x;           // longest causal rows first
   const int hh = blockIdx.y / nch, dc0 = (blockIdx.y % nch) * DVC;
   const int b = blockIdx.z;
   const int T = p.T;
-  const int q0 = qt * FWD_BM, qw0 = q0 + wave * 32;
-  const int qrow = qw0 + c32;
+  const int q0 = qt * BM, qw0 = q0 + wave * 32;
+  int qrow = qw0 + c32;
 
   const E* gq = reinterpret_cast<const E*>(p.q.p) + b * p.q.sb + hh * p.q.sh;
   const E* gk = reinterpret_cast<const E*>(p.k.p) + b * p.k.sb + hh * p.k.sh;
@@ -82,14 +209,31 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(FwdParams p) {
 #pragma unroll
   for (int i = 0; i < N; ++i) coef[i] = p.coef[hh * N + i];
 
-  // Q fragments (B operand of S^T = K Q^T) live in registers for the whole sweep
-  frag qf[N][NSQ];
+  frag qf[QREG ? N : 1][QREG ? NSQ : 1];
+  if constexpr (QREG) {
 #pragma unroll
-  for (int i = 0; i < N; ++i)
+    for (int i = 0; i < N; ++i)
 #pragma unroll
-    for (int s = 0; s < NSQ; ++s)
-      qf[i][s] = qrow < T ? O::load_global(gq + (int64_t)qrow * p.q.st + i * p.q.si + s * KS + hf * O::KH)
-                          : O::zero();
+      for (int s = 0; s < NSQ; ++s)
+        qf[i][s] = qrow < T ? O::load_global(gq + (int64_t)qrow * p.q.st + i * p.q.si + s * KS + hf * O::KH)
+                            : O::zero();
+  } else {
+#pragma unroll
+    for (int i = 0; i < N; ++i) stage<E, HS, BM, HS, NTHR>(Qs + i * BM * HS, gq + i * p.q.si, p.q.st, q0, T - 1, tid);
+  }
+
+  const int kend = min(T, q0 + BM);
+  const int ntiles = (kend + BN - 1) / BN;
+  auto stage_kv = [&](int kt, int buf) {
+    const int k0 = kt * BN;
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+      stage<E, HS, BN, HS, NTHR>(Kb + (buf * N + i) * BN * HS, gk + i * p.k.si, p.k.st, k0, T - 1, tid);
+    stage<E, DVC, BN, DVC, NTHR>(Vb + buf * BN * DVC, gv, p.v.st, k0, T - 1, tid);
+  };
+  stage_kv(0, 0);
+  wait_dma();
+  __syncthreads();
 
   f32x16 acc[N][NDB];
   float m[N], l[N];
@@ -100,103 +244,99 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(FwdParams p) {
 #pragma unroll
     for (int d = 0; d < NDB; ++d) acc[i][d] = f32x16{};
   }
-
-  const int kend = min(T, q0 + FWD_BM);
-  const int ntiles = (kend + BN - 1) / BN;
   const bool wave_live = qw0 < T;
 
   for (int kt = 0; kt < ntiles; ++kt) {
+    // keep lane-derived addresses loop-variant: recomputed per tile instead of
+    // hoisted into (spilled) registers across the whole loop
+    asm volatile("" : "+v"(lane));
+    tid = (wave << 6) + lane; hf = lane >> 5; c32 = lane & 31;
+    qrow = qw0 + c32;
+    const int buf = kt & 1;
+    if (kt + 1 < ntiles) stage_kv(kt + 1, buf ^ 1);
     const int k0 = kt * BN;
-    __syncthreads();
-    // ---- stage K_i tiles and the V chunk into LDS
-    {
-      constexpr int KCH = HS / VEC;
-      constexpr int NKC = N * BN * KCH;
-      for (int c = tid; c < NKC; c += 256) {
-        const int i = c / (BN * KCH), rem = c % (BN * KCH);
-        const int r = rem / KCH, cc = rem % KCH;
-        const int key = k0 + r;
-        stage_vec<E>(Ks + (i * BN + r) * KSTR + cc * VEC,
-                     gk + (int64_t)key * p.k.st + i * p.k.si + cc * VEC, key < T);
-      }
-      constexpr int VCH = DVC / VEC;
-      for (int c = tid; c < BN * VCH; c += 256) {
-        const int r = c / VCH, cc = c % VCH;
-        const int key = k0 + r;
-        stage_vec<E>(Vs + r * VSTR + cc * VEC, gv + (int64_t)key * p.v.st + cc * VEC, key < T);
-      }
-    }
-    __syncthreads();
-    if (!wave_live || k0 > qw0 + 31) continue;      // tile entirely above this wave's diagonal
-
-    const bool needmask = (k0 + BN - 1 > qw0) || (k0 + BN > T);
-    frag pf[N][NKB * SPB];
+    if (wave_live && k0 <= qw0 + 31) {
+      const E* Kc = Kb + buf * N * BN * HS;
+      const E* Vc = Vb + buf * BN * DVC;
+      const bool needmask = (k0 + BN - 1 > qw0) || (k0 + BN > T);
+      frag pf[N][NKB * SPB];
 #pragma unroll
-    for (int i = 0; i < N; ++i) {
-      f32x16 sa[NKB];
+      for (int i = 0; i < N; ++i) {
+        f32x16 sa[NKB];
+        const E* Ki = Kc + i * BN * HS;
 #pragma unroll
-      for (int kb = 0; kb < NKB; ++kb) {
-        sa[kb] = f32x16{};
-        const E* krow = Ks + (i * BN + kb * 32 + c32) * KSTR;
+        for (int kb = 0; kb < NKB; ++kb) {
+          sa[kb] = f32x16{};
 #pragma unroll
-        for (int s = 0; s < NSQ; ++s) sa[kb] = O::mma(O::row(krow, s, hf), qf[i][s], sa[kb]);
-      }
-      if (needmask) {
+          for (int s = 0; s < NSQ; ++s) {
+            frag qb;
+            if constexpr (QREG) qb = qf[i][s];
+            else qb = QI::row(Qs + i * BM * HS, wave * 32 + c32, s, hf);
+            sa[kb] = O::mma(KI::row(Ki, kb * 32 + c32, s, hf), qb, sa[kb]);
+          }
+        }
+        if (needmask) {
+#pragma unroll
+          for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int key = k0 + kb * 32 + rowof(r, hf);
+              if (key > qrow || key >= T) sa[kb][r] = -INFINITY;
+            }
+        }
+        float mx = -INFINITY;
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+          for (int r = 0; r < 16; r += 2) mx = fmaxf(mx, fmaxf(sa[kb][r], sa[kb][r + 1]));
+        mx = wave_max_halves(mx) * p.sl2;
+        if (__any(mx > m[i] + THR)) {          // rescale only when some row's max grew by > 2^THR
+          const float mnew = fmaxf(m[i], mx);
+          const float alpha = exp2_fast(m[i] - mnew);
+          m[i] = mnew;
+          l[i] *= alpha;
+#pragma unroll
+          for (int d = 0; d < NDB; ++d) acc[i][d] *= alpha;
+        }
+        const float mi = m[i];
+        float ls = 0.f;
 #pragma unroll
         for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
-            const int key = k0 + kb * 32 + rowof(r, hf);
-            if (key > qrow || key >= T) sa[kb][r] = -INFINITY;
+            const float e = exp2_fast(fmaf(sa[kb][r], p.sl2, -mi));
+            sa[kb][r] = e;
+            ls += e;
           }
-      }
-      float mx = -INFINITY;
+        l[i] += ls;
 #pragma unroll
-      for (int kb = 0; kb < NKB; ++kb)
+        for (int kb = 0; kb < NKB; ++kb) {
+          if constexpr (SPB == 2) {
+            pf[i][kb * 2 + 0] = O::template pack<0>(sa[kb]);
+            pf[i][kb * 2 + 1] = O::template pack<1>(sa[kb]);
+          } else {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sa[kb][r]);
-      mx = wave_max_halves(mx);
-      const float mnew = fmaxf(m[i], mx * p.sl2);
-      const float alpha = exp2_fast(m[i] - mnew);
-      m[i] = mnew;
-      float ls = 0.f;
-#pragma unroll
-      for (int kb = 0; kb < NKB; ++kb)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float e = exp2_fast(fmaf(sa[kb][r], p.sl2, -mnew));
-          sa[kb][r] = e;
-          ls += e;
-        }
-      l[i] = fmaf(l[i], alpha, ls);
-#pragma unroll
-      for (int d = 0; d < NDB; ++d) acc[i][d] *= alpha;
-#pragma unroll
-      for (int kb = 0; kb < NKB; ++kb) {
-        if constexpr (SPB == 2) {
-          pf[i][kb * 2 + 0] = O::template pack<0>(sa[kb]);
-          pf[i][kb * 2 + 1] = O::template pack<1>(sa[kb]);
-        } else {
-#pragma unroll
-          for (int s = 0; s < 16; ++s) pf[i][kb * SPB + s] = sa[kb][s];
+            for (int s = 0; s < 16; ++s) pf[i][kb * SPB + s] = sa[kb][s];
+          }
         }
       }
+      // O_i^T += V^T P_i^T, one V fragment feeds every branch
+#pragma unroll
+      for (int d = 0; d < NDB; ++d)
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+          for (int s = 0; s < SPB; ++s) {
+            const frag va = VI::tr_perm(Vc, kb * 32, s, hf, d * 32, lane);
+#pragma unroll
+            for (int i = 0; i < N; ++i) acc[i][d] = O::mma(va, pf[i][kb * SPB + s], acc[i][d]);
+          }
     }
-    // ---- O_i^T += V^T P_i^T, the V fragment shared by all branches
-#pragma unroll
-    for (int d = 0; d < NDB; ++d)
-#pragma unroll
-      for (int kb = 0; kb < NKB; ++kb)
-#pragma unroll
-        for (int s = 0; s < SPB; ++s) {
-          const frag va = O::tr_perm(Vs + (kb * 32) * VSTR + d * 32, VSTR, s, hf, lane);
-#pragma unroll
-          for (int i = 0; i < N; ++i) acc[i][d] = O::mma(va, pf[i][kb * SPB + s], acc[i][d]);
-        }
+    wait_dma();
+    __syncthreads();
   }
 
   if (!wave_live || qrow >= T) return;
-  // ---- epilogue: normalise, combine, store O, O_i and LSE
   float inv[N];
 #pragma unroll
   for (int i = 0; i < N; ++i) {
@@ -225,216 +365,391 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(FwdParams p) {
     }
 }
 
-// ------------------------------------------------------------- backward ---
-template <class E> struct BwdWaves { static constexpr int v = 4; };
-template <> struct BwdWaves<float> { static constexpr int v = 2; };
-
-template <class E, int HS, int N, int DV>
-struct BwdSmem {
-  static constexpr int NW = BwdWaves<E>::v;
-  static constexpr int BK = NW * 32;
+// ------------------------------------------------------ backward: dQ ---
+template <class E, int HS, int N, int DV, int NW, bool QREG>
+struct DqCfg {
+  static constexpr int BN = FwdTile<E>::BN;
+  static constexpr int BM = NW * 32;
   static constexpr int HSP = HS < 32 ? 32 : HS;
-  static constexpr int KSTR = HSP + Pad<E>::v;
-  static constexpr int QSTR = HSP + Pad<E>::v;
-  static constexpr int DOSTR = DV + Pad<E>::v;
-  static constexpr int DSSTR = 32 + Pad<E>::v;
-  static constexpr int nK = N * BK * KSTR, nQ = N * 32 * QSTR, nDO = 32 * DOSTR, nDS = N * BK * DSSTR;
-  static constexpr int bytes = (nK + nQ + nDO + nDS) * (int)sizeof(E) + 2 * N * 32 * 4;
+  static constexpr int nQ = QREG ? 0 : N * BM * HS;
+  static constexpr int nK = N * BN * HSP;
+  static constexpr int nV = BN * DV;
+  static constexpr int bytes = (nQ + 2 * nK + 2 * nV) * (int)sizeof(E);
 };
 
-// accumulator budget -> whether dK/dQ and dV are computed by one launch
-template <class E, int HS, int N, int DV>
-struct BwdSplit {
-  static constexpr int HSP = HS < 32 ? 32 : HS;
-  static constexpr bool fused = (N * HSP / 2 + DV / 2) <= 160;
+template <class E, int HS, int N>
+struct DqPick {
+  static constexpr int LIM = 160 * 1024;
+  static constexpr bool q8 = sizeof(E) == 2 && DqCfg<E, HS, N, 2 * HS, 8, false>::bytes <= LIM;
+  static constexpr int NW = q8 ? 8 : (sizeof(E) == 2 ? 4 : 2);
+  static constexpr bool QREG = !q8;
+  static constexpr bool ok = DqCfg<E, HS, N, 2 * HS, NW, QREG>::bytes <= LIM;
 };
 
-template <class E, int HS, int N, int DV, bool DKQ, bool DVV>
-__global__ __launch_bounds__(BwdWaves<E>::v * 64, 1) void attn_bwd_kernel(BwdParams p) {
+template <class E, int HS, int N, int DV, int NW, bool QREG, bool OUTF32>
+__global__ __launch_bounds__(NW * 64, 2) void attn_dq_kernel(BwdParams p) {
   using O = Ops<E>;
   using frag = typename O::frag;
-  using SM = BwdSmem<E, HS, N, DV>;
-  constexpr int NW = SM::NW, BK = SM::BK, HSP = SM::HSP;
-  constexpr int KSTR = SM::KSTR, QSTR = SM::QSTR, DOSTR = SM::DOSTR, DSSTR = SM::DSSTR;
+  using CF = DqCfg<E, HS, N, DV, NW, QREG>;
+  using QI = Img<E, HS>;
+  constexpr int HSP = CF::HSP;
+  using KI = Img<E, HSP>;
+  using VI = Img<E, DV>;
+  constexpr int BN = CF::BN, BM = CF::BM, NTHR = NW * 64;
   constexpr int KS = O::KSTEP;
-  constexpr int VEC = O::VEC;
-  constexpr int NTHR = NW * 64;
-  constexpr int NSQ = HS / KS;         // k-steps over head dim
-  constexpr int NSV = DV / KS;         // k-steps over dv
-  constexpr int SPB = 32 / KS;         // k-steps over a 32-row query tile
-  constexpr int NHB = HSP / 32;
-  constexpr int NVB = DV / 32;
+  constexpr int NSQ = HS / KS, NSV = DV / KS;
+  constexpr int NKB = BN / 32, SPB = 32 / KS, NHB = HSP / 32;
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  E* Ks = reinterpret_cast<E*>(smem);
-  E* Qs = Ks + SM::nK;
-  E* dOs = Qs + SM::nQ;
-  E* dSs = dOs + SM::nDO;
-  float* lse_s = reinterpret_cast<float*>(dSs + SM::nDS);
-  float* del_s = lse_s + N * 32;
+  E* Qs = reinterpret_cast<E*>(smem);   // [N][BM][HS] unless QREG
+  E* Kb = Qs + CF::nQ;                  // [2][N][BN][HSP]
+  E* Vb = Kb + 2 * CF::nK;              // [2][BN][DV]
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int hf = lane >> 5, c32 = lane & 31;
-  const int kblk = blockIdx.x;                // block 0 has the most query tiles: launched first
+  const int wave = threadIdx.x >> 6;
+  int tid = threadIdx.x, lane = tid & 63;
+  int hf = lane >> 5, c32 = lane & 31;
+  const int qt = gridDim.x - 1 - blockIdx.x;
   const int hh = blockIdx.y, b = blockIdx.z;
   const int T = p.T;
-  const int kb0 = kblk * BK, kw0 = kb0 + wave * 32;
-  const int krow = kw0 + c32;
+  const int q0 = qt * BM, qw0 = q0 + wave * 32;
+  int qrow = qw0 + c32;
+  const bool rowok = qrow < T;
 
   const E* gq = reinterpret_cast<const E*>(p.q.p) + b * p.q.sb + hh * p.q.sh;
   const E* gk = reinterpret_cast<const E*>(p.k.p) + b * p.k.sb + hh * p.k.sh;
   const E* gv = reinterpret_cast<const E*>(p.v.p) + b * p.v.sb + hh * p.v.sh;
   const E* gdo = reinterpret_cast<const E*>(p.dout.p) + b * p.dout.sb + hh * p.dout.sh;
+  const E* gob = reinterpret_cast<const E*>(p.obr.p) + b * p.obr.sb + hh * p.obr.sh;
+
+  const int kend = min(T, q0 + BM);
+  const int ntiles = (kend + BN - 1) / BN;
+  auto stage_kv = [&](int kt, int buf) {
+    const int k0 = kt * BN;
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+      stage<E, HSP, BN, HS, NTHR>(Kb + (buf * N + i) * BN * HSP, gk + i * p.k.si, p.k.st, k0, T - 1, tid);
+    stage<E, DV, BN, DV, NTHR>(Vb + buf * BN * DV, gv, p.v.st, k0, T - 1, tid);
+  };
+
+  // ---- per-row operands in registers: Q_i and dO rows (B operands), LSE, delta
+  frag qf[QREG ? N : 1][QREG ? NSQ : 1], df[NSV];
+  float coef[N], lse[N], del[N];
+  const int64_t rs = (((int64_t)0 * p.B + b) * p.H + hh) * T + qrow;     // [i][b][h][t], i = 0
+  const int64_t bstride = (int64_t)p.B * p.H * T;
+#pragma unroll
+  for (int s = 0; s < NSV; ++s)
+    df[s] = rowok ? O::load_global(gdo + (int64_t)qrow * p.dout.st + s * KS + hf * O::KH) : O::zero();
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    coef[i] = p.coef[hh * N + i];
+    if constexpr (QREG) {
+#pragma unroll
+      for (int s = 0; s < NSQ; ++s)
+        qf[i][s] = rowok ? O::load_global(gq + (int64_t)qrow * p.q.st + i * p.q.si + s * KS + hf * O::KH)
+                         : O::zero();
+    }
+    lse[i] = rowok ? p.lse[rs + i * bstride] : 0.f;
+    // delta_i = <dO, O_i> over this row (flash-backward preprocess), both lane halves
+    float d = 0.f;
+    if (rowok) {
+#pragma unroll
+      for (int s = 0; s < NSV; ++s) {
+        const frag o = O::load_global(gob + (int64_t)qrow * p.obr.st + i * p.obr.si + s * KS + hf * O::KH);
+        if constexpr (sizeof(E) == 2) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) d = fmaf((float)df[s][j], (float)o[j], d);
+        } else {
+          d = fmaf(df[s], o, d);
+        }
+      }
+    }
+    d += __shfl_xor(d, 32, 64);
+    del[i] = d;
+    if (rowok && hf == 0) p.delta[rs + i * bstride] = d;
+    // d(coef)[h][i] = sum over rows of delta_i: one atomic per wave
+    float w = (rowok && hf == 0) ? d : 0.f;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) w += __shfl_xor(w, o, 64);
+    if (lane == 0 && qw0 < T) atomicAdd(p.dcoef + hh * N + i, w);
+  }
+
+  if constexpr (!QREG) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) stage<E, HS, BM, HS, NTHR>(Qs + i * BM * HS, gq + i * p.q.si, p.q.st, q0, T - 1, tid);
+  }
+  stage_kv(0, 0);
+  wait_dma();
+  __syncthreads();
+
+  f32x16 dq[N][NHB];
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+#pragma unroll
+    for (int d = 0; d < NHB; ++d) dq[i][d] = f32x16{};
+  const bool wave_live = qw0 < T;
+
+  for (int kt = 0; kt < ntiles; ++kt) {
+    // keep lane-derived addresses loop-variant: recomputed per tile instead of
+    // hoisted into (spilled) registers across the whole loop
+    asm volatile("" : "+v"(lane));
+    tid = (wave << 6) + lane; hf = lane >> 5; c32 = lane & 31;
+    qrow = qw0 + c32;
+    const int buf = kt & 1;
+    if (kt + 1 < ntiles) stage_kv(kt + 1, buf ^ 1);
+    const int k0 = kt * BN;
+    if (wave_live && k0 <= qw0 + 31) {
+      const E* Kc = Kb + buf * N * BN * HSP;
+      const E* Vc = Vb + buf * BN * DV;
+      const bool needmask = (k0 + BN - 1 > qw0) || (k0 + BN > T);
+      f32x16 dp[NKB];
+#pragma unroll
+      for (int kb = 0; kb < NKB; ++kb) {
+        dp[kb] = f32x16{};
+#pragma unroll
+        for (int s = 0; s < NSV; ++s) dp[kb] = O::mma(VI::row(Vc, kb * 32 + c32, s, hf), df[s], dp[kb]);
+      }
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        const E* Ki = Kc + i * BN * HSP;
+        f32x16 sa[NKB];
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb) {
+          sa[kb] = f32x16{};
+#pragma unroll
+          for (int s = 0; s < NSQ; ++s) {
+            frag qb;
+            if constexpr (QREG) qb = qf[i][s];
+            else qb = QI::row(Qs + i * BM * HS, wave * 32 + c32, s, hf);
+            sa[kb] = O::mma(KI::row(Ki, kb * 32 + c32, s, hf), qb, sa[kb]);
+          }
+        }
+        const float li = lse[i], di = del[i], ci = coef[i];
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            float pr = exp2_fast(fmaf(sa[kb][r], p.sl2, -li));
+            if (needmask) {
+              const int key = k0 + kb * 32 + rowof(r, hf);
+              if (key > qrow || key >= T) pr = 0.f;
+            }
+            sa[kb][r] = ci * pr * (dp[kb][r] - di);
+          }
+        // dQ_i^T += K_i^T dS_i^T
+#pragma unroll
+        for (int d = 0; d < NHB; ++d)
+#pragma unroll
+          for (int kb = 0; kb < NKB; ++kb) {
+            if constexpr (SPB == 2) {
+              dq[i][d] = O::mma(KI::tr_perm(Ki, kb * 32, 0, hf, d * 32, lane), O::template pack<0>(sa[kb]), dq[i][d]);
+              dq[i][d] = O::mma(KI::tr_perm(Ki, kb * 32, 1, hf, d * 32, lane), O::template pack<1>(sa[kb]), dq[i][d]);
+            } else {
+#pragma unroll
+              for (int s = 0; s < SPB; ++s)
+                dq[i][d] = O::mma(KI::tr_perm(Ki, kb * 32, s, hf, d * 32, lane), sa[kb][s], dq[i][d]);
+            }
+          }
+      }
+    }
+    wait_dma();
+    __syncthreads();
+  }
+
+  if (!rowok) return;
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+#pragma unroll
+    for (int d = 0; d < NHB; ++d)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int e = d * 32 + 8 * g + 4 * hf;
+        if (e >= HS) continue;
+        const float a0 = dq[i][d][4 * g] * p.scale, a1 = dq[i][d][4 * g + 1] * p.scale;
+        const float a2 = dq[i][d][4 * g + 2] * p.scale, a3 = dq[i][d][4 * g + 3] * p.scale;
+        if constexpr (OUTF32) {
+          store4<float>(p.dq32 + ((((int64_t)b * T + qrow) * p.H + hh) * N + i) * HS + e, a0, a1, a2, a3);
+        } else {
+          E* gdq = reinterpret_cast<E*>(p.dq.p) + b * p.dq.sb + (int64_t)qrow * p.dq.st + hh * p.dq.sh + i * p.dq.si;
+          store4<E>(gdq + e, a0, a1, a2, a3);
+        }
+      }
+}
+
+// --------------------------------------------------- backward: dK, dV ---
+template <class E> struct DkdvWaves { static constexpr int v = 8; };
+template <> struct DkdvWaves<float> { static constexpr int v = 4; };
+
+template <class E, int HS, int N, int DV, int NW>
+struct DkdvCfg {
+  static constexpr int BQ = 32;
+  static constexpr int BK = NW * 32;
+  static constexpr int HSP = HS < 32 ? 32 : HS;
+  static constexpr int NP = (N * BQ + 63) / 64 * 64;      // fp32 row vectors, padded to DMA pieces
+  static constexpr int nQ = N * BQ * HSP;
+  static constexpr int nD = BQ * DV;
+  static constexpr int nK = N * BK * HS;                   // the workgroup's K_i rows (B of S_i)
+  static constexpr int bytes = (nK + 2 * nQ + 2 * nD) * (int)sizeof(E) + 2 * 2 * NP * 4;
+};
+
+// accumulator budget -> whether dK and dV share one launch
+template <int HS, int N, int DV>
+struct DkdvSplit {
+  static constexpr int HSP = HS < 32 ? 32 : HS;
+  static constexpr bool fused = (N * HSP / 2 + DV / 2) <= 160;
+};
+
+template <class E, int HS, int N, int DV, int NW, bool DK, bool DVV>
+__global__ __launch_bounds__(NW * 64, (NW >= 8 ? 2 : 1)) void attn_dkdv_kernel(BwdParams p) {
+  using O = Ops<E>;
+  using frag = typename O::frag;
+  using CF = DkdvCfg<E, HS, N, DV, NW>;
+  constexpr int HSP = CF::HSP, BQ = CF::BQ, BK = CF::BK, NP = CF::NP, NTHR = NW * 64;
+  using QI = Img<E, HSP>;
+  using DI = Img<E, DV>;
+  constexpr int KS = O::KSTEP;
+  constexpr int NSQ = HS / KS, NSV = DV / KS, SPB = 32 / KS;
+  constexpr int NHB = HSP / 32, NVB = DV / 32;
+
+  using KI = Img<E, HS>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  E* Ks = reinterpret_cast<E*>(smem);     // [N][BK][HS]
+  E* Qb = Ks + CF::nK;                    // [2][N][BQ][HSP]
+  E* Db = Qb + 2 * CF::nQ;                // [2][BQ][DV]
+  float* Lb = reinterpret_cast<float*>(Db + 2 * CF::nD);   // [2][NP] lse
+  float* Gb = Lb + 2 * NP;                                  // [2][NP] delta
+
+  const int wave = threadIdx.x >> 6;
+  int tid = threadIdx.x, lane = tid & 63;
+  int hf = lane >> 5, c32 = lane & 31;
+  const int kblk = blockIdx.x;            // block 0 has the most query tiles: dispatched first
+  const int hh = blockIdx.y, b = blockIdx.z;
+  const int T = p.T;
+  const int kb0 = kblk * BK, kw0 = kb0 + wave * 32;
+  int krow = kw0 + c32;
+
+  const E* gq = reinterpret_cast<const E*>(p.q.p) + b * p.q.sb + hh * p.q.sh;
+  const E* gk = reinterpret_cast<const E*>(p.k.p) + b * p.k.sb + hh * p.k.sh;
+  const E* gv = reinterpret_cast<const E*>(p.v.p) + b * p.v.sb + hh * p.v.sh;
+  const E* gdo = reinterpret_cast<const E*>(p.dout.p) + b * p.dout.sb + hh * p.dout.sh;
+  const int64_t rowvec = ((int64_t)b * p.H + hh) * T;       // [i][b][h][t] offset of (b, h)
+  const int64_t bstride = (int64_t)p.B * p.H * T;
 
   float coef[N];
 #pragma unroll
   for (int i = 0; i < N; ++i) coef[i] = p.coef[hh * N + i];
-
-  // ---- the workgroup's key block of every K_i, head dim zero-padded to HSP
-  {
-    constexpr int KCH = HSP / VEC;
-    for (int c = tid; c < N * BK * KCH; c += NTHR) {
-      const int i = c / (BK * KCH), rem = c % (BK * KCH);
-      const int r = rem / KCH, cc = rem % KCH;
-      const int key = kb0 + r;
-      stage_vec<E>(Ks + (i * BK + r) * KSTR + cc * VEC,
-                   gk + (int64_t)key * p.k.st + i * p.k.si + cc * VEC, key < T && cc * VEC < HS);
-    }
+  // this wave's key rows of every K_i and of V as B fragments
+  // this wave's V rows as B fragments of dP = dO V^T (registers); K_i rows live in LDS
+  frag vf[DK ? NSV : 1];
+  if constexpr (DK) {
+#pragma unroll
+    for (int s = 0; s < NSV; ++s)
+      vf[s] = krow < T ? O::load_global(gv + (int64_t)krow * p.v.st + s * KS + hf * O::KH) : O::zero();
   }
-  // ---- this wave's V rows as B fragments of dP = dO V^T
-  frag vf[NSV];
-#pragma unroll
-  for (int s = 0; s < NSV; ++s)
-    vf[s] = (DKQ && krow < T) ? O::load_global(gv + (int64_t)krow * p.v.st + s * KS + hf * O::KH) : O::zero();
 
-  f32x16 dk[DKQ ? N : 1][NHB];
-  f32x16 dvacc[DVV ? NVB : 1];
+  auto stage_q = [&](int q0, int buf) {
 #pragma unroll
-  for (int i = 0; i < (DKQ ? N : 1); ++i)
+    for (int i = 0; i < N; ++i)
+      stage<E, HSP, BQ, HS, NTHR>(Qb + (buf * N + i) * BQ * HSP, gq + i * p.q.si, p.q.st, q0, T - 1, tid);
+    stage<E, DV, BQ, DV, NTHR>(Db + buf * BQ * DV, gdo, p.dout.st, q0, T - 1, tid);
+    stage_rows<N, BQ, NTHR>(Lb + buf * NP, p.lse + rowvec, bstride, q0, T - 1, tid);
+    if constexpr (DK) stage_rows<N, BQ, NTHR>(Gb + buf * NP, p.delta + rowvec, bstride, q0, T - 1, tid);
+  };
+
+  f32x16 dk[DK ? N : 1][NHB];
+  f32x16 dv[DVV ? NVB : 1];
+#pragma unroll
+  for (int i = 0; i < (DK ? N : 1); ++i)
 #pragma unroll
     for (int d = 0; d < NHB; ++d) dk[i][d] = f32x16{};
 #pragma unroll
-  for (int d = 0; d < (DVV ? NVB : 1); ++d) dvacc[d] = f32x16{};
+  for (int d = 0; d < (DVV ? NVB : 1); ++d) dv[d] = f32x16{};
 
-  const bool wave_keys = kw0 < T;
-  for (int q0 = kb0; q0 < T; q0 += 32) {
-    __syncthreads();
-    {
-      constexpr int QCH = HSP / VEC;
-      for (int c = tid; c < N * 32 * QCH; c += NTHR) {
-        const int i = c / (32 * QCH), rem = c % (32 * QCH);
-        const int r = rem / QCH, cc = rem % QCH;
-        const int q = q0 + r;
-        stage_vec<E>(Qs + (i * 32 + r) * QSTR + cc * VEC,
-                     gq + (int64_t)q * p.q.st + i * p.q.si + cc * VEC, q < T && cc * VEC < HS);
-      }
-      constexpr int OCH = DV / VEC;
-      for (int c = tid; c < 32 * OCH; c += NTHR) {
-        const int r = c / OCH, cc = c % OCH;
-        const int q = q0 + r;
-        stage_vec<E>(dOs + r * DOSTR + cc * VEC, gdo + (int64_t)q * p.dout.st + cc * VEC, q < T);
-      }
-      for (int c = tid; c < N * 32; c += NTHR) {
-        const int i = c / 32, r = c % 32, q = q0 + r;
-        const int64_t off = (((int64_t)i * p.B + b) * p.H + hh) * T + q;
-        lse_s[c] = q < T ? p.lse[off] : 0.f;
-        del_s[c] = q < T ? p.delta[off] : 0.f;
-      }
-    }
-    __syncthreads();
-    const bool live = wave_keys && (q0 + 31 >= kw0);
-    if (live) {
-      const bool needmask = (kw0 + 31 > q0) || (q0 + 32 > T) || (kw0 + 32 > T);
-      f32x16 dp = f32x16{};
-      if constexpr (DKQ) {
+  const int ntiles = kb0 < T ? (T - kb0 + BQ - 1) / BQ : 0;
 #pragma unroll
-        for (int s = 0; s < NSV; ++s) dp = O::mma(O::row(dOs + c32 * DOSTR, s, hf), vf[s], dp);
+  for (int i = 0; i < N; ++i) stage<E, HS, BK, HS, NTHR>(Ks + i * BK * HS, gk + i * p.k.si, p.k.st, kb0, T - 1, tid);
+  if (ntiles > 0) stage_q(kb0, 0);
+  wait_dma();
+  __syncthreads();
+  const bool wave_keys = kw0 < T;
+
+  for (int t = 0; t < ntiles; ++t) {
+    // keep lane-derived addresses loop-variant: recomputed per tile instead of
+    // hoisted into (spilled) registers across the whole loop
+    asm volatile("" : "+v"(lane));
+    tid = (wave << 6) + lane; hf = lane >> 5; c32 = lane & 31;
+    krow = kw0 + c32;
+    const int buf = t & 1;
+    const int q0 = kb0 + t * BQ;
+    if (t + 1 < ntiles) stage_q(q0 + BQ, buf ^ 1);
+    if (wave_keys && q0 + BQ - 1 >= kw0) {
+      const E* Qc = Qb + buf * N * BQ * HSP;
+      const E* Dc = Db + buf * BQ * DV;
+      const float* Lc = Lb + buf * NP;
+      const float* Gc = Gb + buf * NP;
+      const bool needmask = (kw0 + 31 > q0) || (q0 + BQ > T) || (kw0 + 32 > T);
+      f32x16 dpa = f32x16{};
+      if constexpr (DK) {
+#pragma unroll
+        for (int s = 0; s < NSV; ++s) dpa = O::mma(DI::row(Dc, c32, s, hf), vf[s], dpa);
       }
       f32x16 pc = f32x16{};
 #pragma unroll
       for (int i = 0; i < N; ++i) {
         f32x16 sa = f32x16{};
-        const E* qrowp = Qs + (i * 32 + c32) * QSTR;
-        const E* krowp = Ks + (i * BK + wave * 32 + c32) * KSTR;
+        const E* Qi = Qc + i * BQ * HSP;
 #pragma unroll
-        for (int s = 0; s < NSQ; ++s) sa = O::mma(O::row(qrowp, s, hf), O::row(krowp, s, hf), sa);
-        // sa[r] = S[q0 + rowof(r)][krow]  ->  P, dS
+        for (int s = 0; s < NSQ; ++s)
+          sa = O::mma(QI::row(Qi, c32, s, hf), KI::row(Ks + i * BK * HS, wave * 32 + c32, s, hf), sa);
+        // sa[r] = S_i[q0 + rowof(r)][krow]; rows 4g..4g+3 of a lane are consecutive
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int qq = rowof(r, hf);
-          float pr = exp2_fast(fmaf(sa[r], p.sl2, -lse_s[i * 32 + qq]));
-          if (needmask && (krow > q0 + qq || q0 + qq >= T || krow >= T)) pr = 0.f;
-          if constexpr (DVV) pc[r] = fmaf(coef[i], pr, pc[r]);
-          if constexpr (DKQ) sa[r] = coef[i] * pr * (dp[r] - del_s[i * 32 + qq]);
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 l4 = *reinterpret_cast<const f32x4*>(Lc + i * BQ + 8 * g + 4 * hf);
+          f32x4 d4 = f32x4{};
+          if constexpr (DK) d4 = *reinterpret_cast<const f32x4*>(Gc + i * BQ + 8 * g + 4 * hf);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int r = 4 * g + j;
+            float pr = exp2_fast(fmaf(sa[r], p.sl2, -l4[j]));
+            if (needmask) {
+              const int q = q0 + rowof(r, hf);
+              if (krow > q || q >= T || krow >= T) pr = 0.f;
+            }
+            if constexpr (DVV) pc[r] = fmaf(coef[i], pr, pc[r]);
+            if constexpr (DK) sa[r] = coef[i] * pr * (dpa[r] - d4[j]);
+          }
         }
-        if constexpr (DKQ) {
-          // dK_i^T += Q_i^T dS_i
+        if constexpr (DK) {
 #pragma unroll
           for (int d = 0; d < NHB; ++d) {
-            const E* qb = Qs + i * 32 * QSTR + d * 32;
             if constexpr (SPB == 2) {
-              dk[i][d] = O::mma(O::tr_perm(qb, QSTR, 0, hf, lane), O::template pack<0>(sa), dk[i][d]);
-              dk[i][d] = O::mma(O::tr_perm(qb, QSTR, 1, hf, lane), O::template pack<1>(sa), dk[i][d]);
+              dk[i][d] = O::mma(QI::tr_perm(Qi, 0, 0, hf, d * 32, lane), O::template pack<0>(sa), dk[i][d]);
+              dk[i][d] = O::mma(QI::tr_perm(Qi, 0, 1, hf, d * 32, lane), O::template pack<1>(sa), dk[i][d]);
             } else {
 #pragma unroll
-              for (int s = 0; s < SPB; ++s) dk[i][d] = O::mma(O::tr_perm(qb, QSTR, s, hf, lane), sa[s], dk[i][d]);
+              for (int s = 0; s < SPB; ++s) dk[i][d] = O::mma(QI::tr_perm(Qi, 0, s, hf, d * 32, lane), sa[s], dk[i][d]);
             }
           }
-          // dS_i -> LDS image [key][query] for dQ
-          E* dsrow = dSs + (i * BK + wave * 32 + c32) * DSSTR;
-#pragma unroll
-          for (int g = 0; g < 4; ++g)
-            store4_lds<E>(dsrow + 8 * g + 4 * hf, sa[4 * g], sa[4 * g + 1], sa[4 * g + 2], sa[4 * g + 3]);
         }
       }
       if constexpr (DVV) {
 #pragma unroll
         for (int d = 0; d < NVB; ++d) {
-          const E* ob = dOs + d * 32;
           if constexpr (SPB == 2) {
-            dvacc[d] = O::mma(O::tr_perm(ob, DOSTR, 0, hf, lane), O::template pack<0>(pc), dvacc[d]);
-            dvacc[d] = O::mma(O::tr_perm(ob, DOSTR, 1, hf, lane), O::template pack<1>(pc), dvacc[d]);
+            dv[d] = O::mma(DI::tr_perm(Dc, 0, 0, hf, d * 32, lane), O::template pack<0>(pc), dv[d]);
+            dv[d] = O::mma(DI::tr_perm(Dc, 0, 1, hf, d * 32, lane), O::template pack<1>(pc), dv[d]);
           } else {
 #pragma unroll
-            for (int s = 0; s < SPB; ++s) dvacc[d] = O::mma(O::tr_perm(ob, DOSTR, s, hf, lane), pc[s], dvacc[d]);
-          }
-        }
-      }
-    } else if constexpr (DKQ) {
-#pragma unroll
-      for (int i = 0; i < N; ++i) {
-        E* dsrow = dSs + (i * BK + wave * 32 + c32) * DSSTR;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) store4_lds<E>(dsrow + 8 * g + 4 * hf, 0.f, 0.f, 0.f, 0.f);
-      }
-    }
-    if constexpr (DKQ) {
-      __syncthreads();
-      // dQ_i[q][d] = sum_k dS_i[q][k] K_i[k][d] over this block's keys; fp32 atomics across blocks
-      constexpr int NB = N * NHB;
-      for (int bi = wave; bi < NB; bi += NW) {
-        const int i = bi / NHB, d = bi % NHB;
-        f32x16 a = f32x16{};
-        const E* dsb = dSs + i * BK * DSSTR;
-        const E* kbp = Ks + i * BK * KSTR + d * 32;
-#pragma unroll 4
-        for (int s = 0; s < BK / KS; ++s)
-          a = O::mma(O::tr_nat(dsb, DSSTR, s, hf, lane), O::tr_nat(kbp, KSTR, s, hf, lane), a);
-        const int dcol = d * 32 + c32;
-        if (dcol < HS) {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int q = q0 + rowof(r, hf);
-            if (q < T)
-              atomicAdd(p.dq + ((((int64_t)b * T + q) * p.H + hh) * N + i) * HS + dcol, a[r] * p.scale);
+            for (int s = 0; s < SPB; ++s) dv[d] = O::mma(DI::tr_perm(Dc, 0, s, hf, d * 32, lane), pc[s], dv[d]);
           }
         }
       }
     }
+    wait_dma();
+    __syncthreads();
   }
 
   if (!wave_keys || krow >= T) return;
-  if constexpr (DKQ) {
+  if constexpr (DK) {
     E* gdk = reinterpret_cast<E*>(p.dk.p) + b * p.dk.sb + (int64_t)krow * p.dk.st + hh * p.dk.sh;
 #pragma unroll
     for (int i = 0; i < N; ++i)
@@ -455,7 +770,7 @@ __global__ __launch_bounds__(BwdWaves<E>::v * 64, 1) void attn_bwd_kernel(BwdPar
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int e = d * 32 + 8 * g + 4 * hf;
-        store4<E>(gdv + e, dvacc[d][4 * g], dvacc[d][4 * g + 1], dvacc[d][4 * g + 2], dvacc[d][4 * g + 3]);
+        store4<E>(gdv + e, dv[d][4 * g], dv[d][4 * g + 1], dv[d][4 * g + 2], dv[d][4 * g + 3]);
       }
   }
 }
@@ -469,31 +784,60 @@ static inline int set_smem(K kernel, int bytes) {
 }
 
 template <class E, int HS, int N>
+struct Plan {
+  static constexpr int DV = 2 * HS;
+  using FP = FwdPick<E, HS, N>;
+  using DP = DqPick<E, HS, N>;
+  static constexpr int KVW = DkdvWaves<E>::v;
+  static constexpr bool ok = FP::ok && DP::ok && DkdvCfg<E, HS, N, DV, KVW>::bytes <= 160 * 1024;
+};
+
+template <class E, int HS, int N>
 int launch_fwd_t(const FwdParams& p, hipStream_t st) {
-  constexpr int DV = 2 * HS;
-  constexpr int DVC = FwdChunk<N, DV>::DVC;
-  constexpr int bytes = FwdSmem<E, HS, N, DVC>::bytes;
-  auto kern = attn_fwd_kernel<E, HS, N, DVC>;
+  using PL = Plan<E, HS, N>;
+  using FP = typename PL::FP;
+  constexpr int DVC = FP::DVC, NW = FP::NW;
+  constexpr int bytes = FwdCfg<E, HS, N, DVC, NW, FP::QREG>::bytes;
+  auto kern = attn_fwd_kernel<E, HS, N, DVC, NW, FP::QREG>;
   if (int e = set_smem(kern, bytes)) return e;
-  dim3 grid((p.T + FWD_BM - 1) / FWD_BM, p.H * (DV / DVC), p.B);
-  hipLaunchKernelGGL(kern, grid, dim3(256), bytes, st, p);
+  dim3 grid((p.T + NW * 32 - 1) / (NW * 32), p.H * (PL::DV / DVC), p.B);
+  hipLaunchKernelGGL(kern, grid, dim3(NW * 64), bytes, st, p);
   return (int)hipGetLastError();
 }
 
 template <class E, int HS, int N>
-int launch_bwd_t(const BwdParams& p, hipStream_t st) {
-  constexpr int DV = 2 * HS;
-  using SM = BwdSmem<E, HS, N, DV>;
-  constexpr int bytes = SM::bytes;
-  dim3 grid((p.T + SM::BK - 1) / SM::BK, p.H, p.B);
-  dim3 block(SM::NW * 64);
-  if constexpr (BwdSplit<E, HS, N, DV>::fused) {
-    auto kern = attn_bwd_kernel<E, HS, N, DV, true, true>;
+int launch_dq_t(const BwdParams& p, hipStream_t st) {
+  using PL = Plan<E, HS, N>;
+  constexpr int NW = PL::DP::NW, DV = PL::DV;
+  constexpr bool QR = PL::DP::QREG;
+  constexpr int bytes = DqCfg<E, HS, N, DV, NW, QR>::bytes;
+  dim3 grid((p.T + NW * 32 - 1) / (NW * 32), p.H, p.B);
+  if (p.dq32) {
+    auto kern = attn_dq_kernel<E, HS, N, DV, NW, QR, true>;
+    if (int e = set_smem(kern, bytes)) return e;
+    hipLaunchKernelGGL(kern, grid, dim3(NW * 64), bytes, st, p);
+  } else {
+    auto kern = attn_dq_kernel<E, HS, N, DV, NW, QR, false>;
+    if (int e = set_smem(kern, bytes)) return e;
+    hipLaunchKernelGGL(kern, grid, dim3(NW * 64), bytes, st, p);
+  }
+  return (int)hipGetLastError();
+}
+
+template <class E, int HS, int N>
+int launch_dkdv_t(const BwdParams& p, hipStream_t st) {
+  using PL = Plan<E, HS, N>;
+  constexpr int NW = PL::KVW, DV = PL::DV;
+  constexpr int bytes = DkdvCfg<E, HS, N, DV, NW>::bytes;
+  dim3 grid((p.T + NW * 32 - 1) / (NW * 32), p.H, p.B);
+  dim3 block(NW * 64);
+  if constexpr (DkdvSplit<HS, N, DV>::fused) {
+    auto kern = attn_dkdv_kernel<E, HS, N, DV, NW, true, true>;
     if (int e = set_smem(kern, bytes)) return e;
     hipLaunchKernelGGL(kern, grid, block, bytes, st, p);
   } else {
-    auto k1 = attn_bwd_kernel<E, HS, N, DV, true, false>;
-    auto k2 = attn_bwd_kernel<E, HS, N, DV, false, true>;
+    auto k1 = attn_dkdv_kernel<E, HS, N, DV, NW, true, false>;
+    auto k2 = attn_dkdv_kernel<E, HS, N, DV, NW, false, true>;
     if (int e = set_smem(k1, bytes)) return e;
     if (int e = set_smem(k2, bytes)) return e;
     hipLaunchKernelGGL(k1, grid, block, bytes, st, p);
@@ -502,40 +846,41 @@ int launch_bwd_t(const BwdParams& p, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
-template <class E, int HS, int N>
-constexpr bool fits() {
-  return BwdSmem<E, HS, N, 2 * HS>::bytes <= 160 * 1024 &&
-         FwdSmem<E, HS, N, FwdChunk<N, 2 * HS>::DVC>::bytes <= 160 * 1024;
-}
+#define DTA_FOR_CONFIGS(X) \
+  X(16, 1) X(16, 2) X(16, 3) X(16, 4) X(32, 1) X(32, 2) X(32, 3) X(32, 4) \
+  X(64, 1) X(64, 2) X(64, 3) X(64, 4) X(128, 1) X(128, 2) X(128, 3) X(128, 4)
 
 template <class E>
 int dispatch_fwd(const FwdParams& p, hipStream_t st) {
 #define DTA_F(HS_, N_) \
-  if (p.HS == HS_ && p.N == N_) { if constexpr (fits<E, HS_, N_>()) return launch_fwd_t<E, HS_, N_>(p, st); else return -2; }
-#define DTA_FN(HS_) DTA_F(HS_, 1) DTA_F(HS_, 2) DTA_F(HS_, 3) DTA_F(HS_, 4)
-  DTA_FN(16) DTA_FN(32) DTA_FN(64) DTA_FN(128)
-#undef DTA_FN
+  if (p.HS == HS_ && p.N == N_) { if constexpr (Plan<E, HS_, N_>::ok) return launch_fwd_t<E, HS_, N_>(p, st); else return -2; }
+  DTA_FOR_CONFIGS(DTA_F)
 #undef DTA_F
   return -2;
 }
 
 template <class E>
-int dispatch_bwd(const BwdParams& p, hipStream_t st) {
-#define DTA_B(HS_, N_) \
-  if (p.HS == HS_ && p.N == N_) { if constexpr (fits<E, HS_, N_>()) return launch_bwd_t<E, HS_, N_>(p, st); else return -2; }
-#define DTA_BN(HS_) DTA_B(HS_, 1) DTA_B(HS_, 2) DTA_B(HS_, 3) DTA_B(HS_, 4)
-  DTA_BN(16) DTA_BN(32) DTA_BN(64) DTA_BN(128)
-#undef DTA_BN
-#undef DTA_B
+int dispatch_dq(const BwdParams& p, hipStream_t st) {
+#define DTA_Q(HS_, N_) \
+  if (p.HS == HS_ && p.N == N_) { if constexpr (Plan<E, HS_, N_>::ok) return launch_dq_t<E, HS_, N_>(p, st); else return -2; }
+  DTA_FOR_CONFIGS(DTA_Q)
+#undef DTA_Q
+  return -2;
+}
+
+template <class E>
+int dispatch_dkdv(const BwdParams& p, hipStream_t st) {
+#define DTA_K(HS_, N_) \
+  if (p.HS == HS_ && p.N == N_) { if constexpr (Plan<E, HS_, N_>::ok) return launch_dkdv_t<E, HS_, N_>(p, st); else return -2; }
+  DTA_FOR_CONFIGS(DTA_K)
+#undef DTA_K
   return -2;
 }
 
 template <class E>
 bool supported_t(int hs, int n) {
-#define DTA_S(HS_, N_) if (hs == HS_ && n == N_) return fits<E, HS_, N_>();
-#define DTA_SN(HS_) DTA_S(HS_, 1) DTA_S(HS_, 2) DTA_S(HS_, 3) DTA_S(HS_, 4)
-  DTA_SN(16) DTA_SN(32) DTA_SN(64) DTA_SN(128)
-#undef DTA_SN
+#define DTA_S(HS_, N_) if (hs == HS_ && n == N_) return Plan<E, HS_, N_>::ok;
+  DTA_FOR_CONFIGS(DTA_S)
 #undef DTA_S
   return false;
 }

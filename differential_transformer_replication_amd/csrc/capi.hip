@@ -8,9 +8,12 @@ namespace dta {
 int launch_attn_fwd_bf16(const FwdParams&, hipStream_t);
 int launch_attn_fwd_f16(const FwdParams&, hipStream_t);
 int launch_attn_fwd_f32(const FwdParams&, hipStream_t);
-int launch_attn_bwd_bf16(const BwdParams&, hipStream_t);
-int launch_attn_bwd_f16(const BwdParams&, hipStream_t);
-int launch_attn_bwd_f32(const BwdParams&, hipStream_t);
+int launch_attn_dq_bf16(const BwdParams&, hipStream_t);
+int launch_attn_dq_f16(const BwdParams&, hipStream_t);
+int launch_attn_dq_f32(const BwdParams&, hipStream_t);
+int launch_attn_dkdv_bf16(const BwdParams&, hipStream_t);
+int launch_attn_dkdv_f16(const BwdParams&, hipStream_t);
+int launch_attn_dkdv_f32(const BwdParams&, hipStream_t);
 bool attn_supported_bf16(int, int);
 bool attn_supported_f16(int, int);
 bool attn_supported_f32(int, int);
@@ -23,11 +26,19 @@ int launch_attn_fwd(int dtype, const FwdParams& p, hipStream_t st) {
   }
   return -2;
 }
-int launch_attn_bwd(int dtype, const BwdParams& p, hipStream_t st) {
+int launch_attn_dq(int dtype, const BwdParams& p, hipStream_t st) {
   switch (dtype) {
-    case DTA_BF16: return launch_attn_bwd_bf16(p, st);
-    case DTA_F16: return launch_attn_bwd_f16(p, st);
-    case DTA_F32: return launch_attn_bwd_f32(p, st);
+    case DTA_BF16: return launch_attn_dq_bf16(p, st);
+    case DTA_F16: return launch_attn_dq_f16(p, st);
+    case DTA_F32: return launch_attn_dq_f32(p, st);
+  }
+  return -2;
+}
+int launch_attn_dkdv(int dtype, const BwdParams& p, hipStream_t st) {
+  switch (dtype) {
+    case DTA_BF16: return launch_attn_dkdv_bf16(p, st);
+    case DTA_F16: return launch_attn_dkdv_f16(p, st);
+    case DTA_F32: return launch_attn_dkdv_f32(p, st);
   }
   return -2;
 }
@@ -127,40 +138,27 @@ int dta_attn_bwd(const dta_attn_bwd_args* a, void* stream) {
   if (!attn_supported(a->dtype, a->head_size, a->n_terms, a->dv)) return DTA_ERR_UNSUPPORTED;
   if (!a->dcoef) return DTA_ERR_INVALID;
   hipStream_t st = (hipStream_t)stream;
-  if ((int64_t)a->B * a->T == 0) {
-    return status((int)hipMemsetAsync(a->dcoef, 0, sizeof(float) * a->H * a->n_terms, st));
+  const int stages = a->stages ? a->stages : (DTA_BWD_PRE | DTA_BWD_DQ | DTA_BWD_DKDV);
+  if (stages & DTA_BWD_PRE) {
+    if (hipMemsetAsync(a->dcoef, 0, sizeof(float) * a->H * a->n_terms, st)) return DTA_ERR_LAUNCH;
   }
+  if ((int64_t)a->B * a->T == 0) return DTA_OK;
   if (!ok_tensor(a->q, a->dtype, true) || !ok_tensor(a->k, a->dtype, true) || !ok_tensor(a->v, a->dtype, false) ||
       !ok_tensor(a->obr, a->dtype, true) || !ok_tensor(a->dout, a->dtype, false) ||
       !ok_tensor(a->dk, a->dtype, true) || !ok_tensor(a->dv_out, a->dtype, false) ||
-      !a->lse || !a->coef || !a->delta || !aligned_ptr(a->dq_f32))
+      !a->lse || !a->coef || !a->delta)
     return DTA_ERR_INVALID;
-  if (a->dq.ptr && !ok_tensor(a->dq, a->dtype, true)) return DTA_ERR_INVALID;
-  const int B = a->B, T = a->T, H = a->H, N = a->n_terms, HS = a->head_size;
-  const int stages = a->stages ? a->stages : (DTA_BWD_PRE | DTA_BWD_MAIN | DTA_BWD_POST);
-  int e = 0;
-  if (stages & DTA_BWD_PRE) {
-    if (hipMemsetAsync(a->dq_f32, 0, (size_t)B * T * H * N * HS * 4, st)) return DTA_ERR_LAUNCH;
-    DeltaParams dp{};
-    dp.dout = t5(a->dout); dp.obr = t5(a->obr); dp.delta = a->delta;
-    dp.B = B; dp.T = T; dp.H = H; dp.N = N; dp.DV = a->dv;
-    if ((e = launch_delta(a->dtype, dp, st))) return status(e);
-    if ((e = launch_dcoef(a->delta, a->dcoef, B, T, H, N, st))) return status(e);
-  }
-  if (!(stages & DTA_BWD_MAIN)) goto post;
-  {
+  if (a->dq.ptr ? !ok_tensor(a->dq, a->dtype, true) : !aligned_ptr(a->dq_f32)) return DTA_ERR_INVALID;
   BwdParams p{};
-  p.q = t5(a->q); p.k = t5(a->k); p.v = t5(a->v); p.dout = t5(a->dout);
-  p.dk = t5(a->dk); p.dv = t5(a->dv_out);
-  p.lse = a->lse; p.delta = a->delta; p.coef = a->coef; p.dq = a->dq_f32;
-  p.B = B; p.T = T; p.H = H; p.N = N; p.HS = HS; p.DV = a->dv;
+  p.q = t5(a->q); p.k = t5(a->k); p.v = t5(a->v); p.obr = t5(a->obr); p.dout = t5(a->dout);
+  p.dq = t5(a->dq); p.dk = t5(a->dk); p.dv = t5(a->dv_out);
+  p.lse = a->lse; p.delta = a->delta; p.coef = a->coef; p.dcoef = a->dcoef;
+  p.dq32 = a->dq.ptr ? nullptr : a->dq_f32;
+  p.B = a->B; p.T = a->T; p.H = a->H; p.N = a->n_terms; p.HS = a->head_size; p.DV = a->dv;
   p.scale = a->scale; p.sl2 = a->scale * kLog2e;
-  if ((e = launch_attn_bwd(a->dtype, p, st))) return status(e);
-  }
-post:
-  if ((stages & DTA_BWD_POST) && a->dq.ptr) {
-    if ((e = launch_cast(a->dtype, a->dq_f32, t5(a->dq), B, T, H, N, HS, st))) return status(e);
-  }
+  int e = 0;
+  if ((stages & DTA_BWD_DQ) && (e = launch_attn_dq(a->dtype, p, st))) return status(e);
+  if ((stages & DTA_BWD_DKDV) && (e = launch_attn_dkdv(a->dtype, p, st))) return status(e);
   return DTA_OK;
 }
 

@@ -20,18 +20,20 @@ struct FwdParams {
 };
 
 struct BwdParams {
-  T5 q, k, v, dout, dk, dv;
+  T5 q, k, v, obr, dout, dq, dk, dv;
   const float* lse;
-  const float* delta;
+  float* delta;        // written by attn_dq, read by attn_dkdv
   const float* coef;
-  float* dq;           // fp32 [b][t][h][i][d] contiguous
+  float* dcoef;        // accumulated by attn_dq (zeroed first)
+  float* dq32;         // if set: dQ written as fp32 [b][t][h][i][d] instead of into dq
   int B, T, H, N, HS, DV;
   float sl2, scale;
 };
 
 // per-dtype launchers (dtype index: 0 bf16, 1 f16, 2 f32); return hipError_t
 int launch_attn_fwd(int dtype, const FwdParams& p, hipStream_t st);
-int launch_attn_bwd(int dtype, const BwdParams& p, hipStream_t st);
+int launch_attn_dq(int dtype, const BwdParams& p, hipStream_t st);
+int launch_attn_dkdv(int dtype, const BwdParams& p, hipStream_t st);
 bool attn_supported(int dtype, int hs, int n, int dv);
 
 struct LnParams {

@@ -141,8 +141,9 @@ class _DiffAttention(torch.autograd.Function):
         dq, dk, dvv = split_packed(dqkv, H, N, hs, dv)
         dcoef = torch.empty(H, N, device=dev, dtype=torch.float32)
         delta = torch.empty(N, B, H, T, device=dev, dtype=torch.float32)
-        dq32 = torch.empty(B, T, H, N, hs, device=dev, dtype=torch.float32)
         rope = freqs is not None
+        # with RoPE the kernels produce gradients of the ROTATED Q/K; dQ stays fp32 for the inverse rotation
+        dq32 = torch.empty(B, T, H, N, hs, device=dev, dtype=torch.float32) if rope else None
         dk_rot = torch.empty(B, T, H, N, hs, device=dev, dtype=qkv.dtype) if rope else None
         obr_t = _lib.DtaTensor(obr.data_ptr(), *obr.stride()[1:4], obr.stride(0))
         null = _lib.DtaTensor(None, 0, 0, 0, 0)
@@ -151,13 +152,15 @@ class _DiffAttention(torch.autograd.Function):
                              lse.data_ptr(), coef.data_ptr(), _lib.tensor5(do),
                              null if rope else _lib.tensor5(dq),
                              _lib.tensor5(dk_rot if rope else dk), _lib.tensor5(dvv),
-                             dcoef.data_ptr(), delta.data_ptr(), dq32.data_ptr(), _lib.BWD_PRE)
+                             dcoef.data_ptr(), delta.data_ptr(), dq32.data_ptr() if rope else None,
+                             _lib.BWD_PRE)
         _lib.check(lib.dta_attn_bwd(a, stream))
-        a.stages = _lib.BWD_MAIN
-        with TIMER.region("attn_bwd"):
+        a.stages = _lib.BWD_DQ
+        with TIMER.region("attn_bwd_dq"):
             _lib.check(lib.dta_attn_bwd(a, stream))
-        a.stages = _lib.BWD_POST
-        _lib.check(lib.dta_attn_bwd(a, stream))
+        a.stages = _lib.BWD_DKDV
+        with TIMER.region("attn_bwd_dkdv"):
+            _lib.check(lib.dta_attn_bwd(a, stream))
         if rope:
             # gradients back through the rotation: conjugate rotate (Ndiff_transformer.py:11-22 bwd)
             ra = _lib.RopeArgs(dt, B, T, H, N, hs, 1, 1, _lib.tensor5(dq32), _lib.tensor5(dq), freqs.data_ptr())

@@ -79,12 +79,16 @@ int dta_attn_fwd(const dta_attn_fwd_args* a, void* stream);
 
 /* Backward of dta_attn_fwd (the autograd of diff_transformer.py:57-72 and
  * Ndiff_transformer.py:102-125): dQ_i, dK_i, dV and d(coef).  Maps are
- * recomputed from LSE; nothing T x T is stored.  dcoef[h][i] =
- * sum_{b,t} <dO, A_i V> (SURVEY semantic 5), from which autograd reaches
- * lambda_q and lambda_k params through get_lambda (diff_transformer.py:41-48).
+ * recomputed from LSE; nothing T x T is stored and no atomics touch dQ.
+ * Two fused kernels: a query-major one (delta_i = <dO, O_i>, dQ_i, d(coef))
+ * and a key-major one (dK_i, dV).  dcoef[h][i] = sum_{b,t} <dO, A_i V>
+ * (SURVEY semantic 5), from which autograd reaches the lambda_q and lambda_k
+ * params through get_lambda (diff_transformer.py:41-48).
  * Workspaces (caller-allocated, see dta_attn_bwd_workspace_bytes):
  *   delta   fp32 [i][b][h][t]
- *   dq_f32  fp32 [b][t][h][i][d] contiguous (zeroed by the call) */
+ *   dq_f32  optional fp32 [b][t][h][i][d] contiguous: when dq.ptr is NULL the
+ *           dQ kernel writes fp32 here instead (callers that post-process dQ,
+ *           e.g. the inverse RoPE, keep full precision). */
 typedef struct dta_attn_bwd_args {
   int32_t dtype;
   int32_t B, T, H, n_terms, head_size, dv;
@@ -94,17 +98,18 @@ typedef struct dta_attn_bwd_args {
   const float* lse;          /* fp32 [i][b][h][t] from the forward */
   const float* coef;         /* fp32 [h][i] */
   dta_tensor dout;           /* dO [b][t][h][e] */
-  dta_tensor dq, dk, dv_out; /* outputs (dtype); dq is written from dq_f32 */
+  dta_tensor dq, dk, dv_out; /* outputs (dtype) */
   float* dcoef;              /* output fp32 [h][i] (overwritten) */
   float* delta;              /* workspace fp32 [i][b][h][t] */
-  float* dq_f32;             /* workspace fp32 [b][t][h][i][d] */
-  int32_t stages;            /* 0 = all; else bitmask of DTA_BWD_PRE (zero dq_f32,
-                                delta, dcoef), DTA_BWD_MAIN (the fused kernel),
-                                DTA_BWD_POST (dq cast) -- lets a caller bracket
-                                one stage with events on the same stream */
+  float* dq_f32;             /* see above */
+  int32_t stages;            /* 0 = all; else bitmask of DTA_BWD_PRE (zero dcoef),
+                                DTA_BWD_DQ (query-major kernel), DTA_BWD_DKDV
+                                (key-major kernel) -- lets a caller bracket one
+                                kernel with events on the same stream; DQ must
+                                run before DKDV (it produces delta) */
 } dta_attn_bwd_args;
 
-enum { DTA_BWD_PRE = 1, DTA_BWD_MAIN = 2, DTA_BWD_POST = 4 };
+enum { DTA_BWD_PRE = 1, DTA_BWD_DQ = 2, DTA_BWD_DKDV = 4 };
 
 int dta_attn_bwd(const dta_attn_bwd_args* a, void* stream);
 size_t dta_attn_bwd_workspace_bytes(int32_t B, int32_t T, int32_t H, int32_t n_terms,
