@@ -193,10 +193,13 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_kernel(FwdParams p) {
   const int wave = threadIdx.x >> 6;
   int tid = threadIdx.x, lane = tid & 63;
   int hf = lane >> 5, c32 = lane & 31;
+  const int nblk = gridDim.x * gridDim.y * gridDim.z;
+  const int lin = xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z), nblk);
+  const int bx = lin % gridDim.x, by = (lin / gridDim.x) % gridDim.y, bz = lin / (gridDim.x * gridDim.y);
   const int nch = p.DV / DVC;
-  const int qt = gridDim.x - 1 - blockIdx.x;           // longest causal rows first
-  const int hh = blockIdx.y / nch, dc0 = (blockIdx.y % nch) * DVC;
-  const int b = blockIdx.z;
+  const int qt = gridDim.x - 1 - bx;                   // longest causal rows first
+  const int hh = by / nch, dc0 = (by % nch) * DVC;
+  const int b = bz;
   const int T = p.T;
   const int q0 = qt * BM, qw0 = q0 + wave * 32;
   int qrow = qw0 + c32;
@@ -340,7 +343,7 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_kernel(FwdParams p) {
   float inv[N];
 #pragma unroll
   for (int i = 0; i < N; ++i) {
-    const float lt = l[i] + __shfl_xor(l[i], 32, 64);
+    const float lt = wave_sum_halves(l[i]);
     inv[i] = 1.f / lt;
     if (dc0 == 0 && hf == 0)
       p.lse[(((int64_t)i * p.B + b) * p.H + hh) * T + qrow] = m[i] + __builtin_log2f(lt);
@@ -408,8 +411,11 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_dq_kernel(BwdParams p) {
   const int wave = threadIdx.x >> 6;
   int tid = threadIdx.x, lane = tid & 63;
   int hf = lane >> 5, c32 = lane & 31;
-  const int qt = gridDim.x - 1 - blockIdx.x;
-  const int hh = blockIdx.y, b = blockIdx.z;
+  const int nblk = gridDim.x * gridDim.y * gridDim.z;
+  const int lin = xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z), nblk);
+  const int bx = lin % gridDim.x, by = (lin / gridDim.x) % gridDim.y, bz = lin / (gridDim.x * gridDim.y);
+  const int qt = gridDim.x - 1 - bx;
+  const int hh = by, b = bz;
   const int T = p.T;
   const int q0 = qt * BM, qw0 = q0 + wave * 32;
   int qrow = qw0 + c32;
@@ -463,7 +469,7 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_dq_kernel(BwdParams p) {
         }
       }
     }
-    d += __shfl_xor(d, 32, 64);
+    d = wave_sum_halves(d);
     del[i] = d;
     if (rowok && hf == 0) p.delta[rs + i * bstride] = d;
     // d(coef)[h][i] = sum over rows of delta_i: one atomic per wave
@@ -621,8 +627,11 @@ __global__ __launch_bounds__(NW * 64, (NW >= 8 ? 2 : 1)) void attn_dkdv_kernel(B
   const int wave = threadIdx.x >> 6;
   int tid = threadIdx.x, lane = tid & 63;
   int hf = lane >> 5, c32 = lane & 31;
-  const int kblk = blockIdx.x;            // block 0 has the most query tiles: dispatched first
-  const int hh = blockIdx.y, b = blockIdx.z;
+  const int nblk = gridDim.x * gridDim.y * gridDim.z;
+  const int lin = xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z), nblk);
+  const int bx = lin % gridDim.x, by = (lin / gridDim.x) % gridDim.y, bz = lin / (gridDim.x * gridDim.y);
+  const int kblk = bx;                    // block 0 has the most query tiles: dispatched first
+  const int hh = by, b = bz;
   const int T = p.T;
   const int kb0 = kblk * BK, kw0 = kb0 + wave * 32;
   int krow = kw0 + c32;

@@ -30,9 +30,26 @@ __device__ __forceinline__ int rowof(int r, int h) { return (r & 3) + 8 * (r >> 
 
 __device__ __forceinline__ float exp2_fast(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// combine lane l with lane l^32 (the two halves that hold the same column):
+// one v_permlane32_swap (VALU) instead of an LDS bpermute round trip
 __device__ __forceinline__ float wave_max_halves(float v) {
-  // combine lane l with lane l^32 (the two halves that hold the same column)
-  return fmaxf(v, __shfl_xor(v, 32, 64));
+  const unsigned u = __float_as_uint(v);
+  auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float wave_sum_halves(float v) {
+  const unsigned u = __float_as_uint(v);
+  auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+// XCD-aware workgroup order: blocks are dealt round-robin over the 8 XCDs;
+// remap the linear id so each XCD receives a contiguous range (neighbouring
+// tiles of one (batch, head) then share that XCD's L2).  Bijective for any
+// count (cdna_hip_programming.md T1).  Speed only -- never correctness.
+__device__ __forceinline__ int xcd_remap(int id, int n) {
+  const int q = n / 8, r = n % 8, x = id % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + id / 8;
 }
 
 template <class E> struct Ops;

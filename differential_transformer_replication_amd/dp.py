@@ -1,0 +1,125 @@
+"""Data-parallel gradient synchronisation: bucketed all-reduce overlapped with
+backward, one process per GPU over RCCL (``torch.distributed`` backend
+``"nccl"`` is RCCL on ROCm; xGMI between the GPUs of a node).
+
+The reference imports DDP/DistributedSampler but never uses them
+(train.py:7-10, 88, 143-145): this is net-new.
+
+Design
+* Parameters are grouped into buckets in reverse registration order (the order
+  autograd produces their gradients).  Each bucket owns one flat fp32 buffer;
+  every parameter's ``.grad`` is a view into it (gradient-as-bucket-view), so
+  autograd accumulates straight into the buffer and no copy is needed.
+* A post-accumulate-grad hook counts ready gradients per bucket; the last one
+  launches ``all_reduce(SUM, async_op=True)`` on that bucket while backward
+  keeps running on the compute stream (RCCL runs on its own stream, ordered
+  after the producing kernels).
+* ``synchronize()`` (before unscale/clip/step) waits for every bucket and
+  scales by 1/world.  ``no_sync()`` skips communication for gradient
+  accumulation micro-steps.
+* Buffers (``lambda_init``, ``freqs_cis``) are never broadcast per step; the
+  reference's T x T ``tril`` does not exist here (SURVEY semantic 8).
+"""
+from __future__ import annotations
+
+import contextlib
+from typing import Dict, List, Optional
+
+import torch
+import torch.distributed as dist
+
+
+class _Bucket:
+    __slots__ = ("params", "flat", "pending", "handle", "size")
+
+    def __init__(self, params: List[torch.nn.Parameter], flat: torch.Tensor):
+        self.params = params
+        self.flat = flat
+        self.size = len(params)
+        self.pending = self.size
+        self.handle = None
+
+
+class BucketedAllReduce:
+    def __init__(self, module: torch.nn.Module, bucket_cap_mb: float = 64.0,
+                 process_group: Optional[dist.ProcessGroup] = None, broadcast_init: bool = True):
+        self.pg = process_group
+        self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
+        self.params = [p for p in module.parameters() if p.requires_grad]
+        self._enabled = True
+        cap = int(bucket_cap_mb * 1024 * 1024)
+        groups: List[List[torch.nn.Parameter]] = []
+        cur, cur_bytes = [], 0
+        for p in reversed(self.params):
+            nb = p.numel() * 4
+            if cur and cur_bytes + nb > cap:
+                groups.append(cur)
+                cur, cur_bytes = [], 0
+            cur.append(p)
+            cur_bytes += nb
+        if cur:
+            groups.append(cur)
+        self.buckets: List[_Bucket] = []
+        self._owner: Dict[int, _Bucket] = {}
+        for g in groups:
+            dev = g[0].device
+            flat = torch.zeros(sum(p.numel() for p in g), device=dev, dtype=torch.float32)
+            off = 0
+            for p in g:
+                if p.dtype != torch.float32:
+                    raise RuntimeError("bucketed all-reduce expects fp32 master parameters")
+                p.grad = flat[off:off + p.numel()].view_as(p)
+                off += p.numel()
+            b = _Bucket(g, flat)
+            self.buckets.append(b)
+            for p in g:
+                self._owner[id(p)] = b
+        for p in self.params:
+            p.register_post_accumulate_grad_hook(self._on_grad)
+        if broadcast_init and self.world > 1:
+            # identical initial parameters on every rank (parameters only, once)
+            with torch.no_grad():
+                for p in self.params:
+                    dist.broadcast(p.data, src=0, group=self.pg)
+
+    # ----------------------------------------------------------- hooks ---
+    def _on_grad(self, p: torch.nn.Parameter) -> None:
+        if not self._enabled or self.world == 1:
+            return
+        b = self._owner[id(p)]
+        if p.grad is None or p.grad.data_ptr() < b.flat.data_ptr() or \
+                p.grad.data_ptr() >= b.flat.data_ptr() + b.flat.numel() * 4:
+            raise RuntimeError("parameter gradient is no longer a view of its bucket "
+                               "(use BucketedAllReduce.zero_grad, not set_to_none)")
+        b.pending -= 1
+        if b.pending == 0:
+            b.handle = dist.all_reduce(b.flat, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        prev, self._enabled = self._enabled, False
+        try:
+            yield
+        finally:
+            self._enabled = prev
+
+    def synchronize(self) -> None:
+        """Wait for every bucket (launching any whose gradients never all arrived,
+        e.g. unused parameters -- identical on every rank) and average."""
+        if self.world == 1:
+            return
+        for b in self.buckets:
+            if b.handle is None:
+                b.handle = dist.all_reduce(b.flat, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+        inv = 1.0 / self.world
+        for b in self.buckets:
+            b.handle.wait()
+            b.flat.mul_(inv)
+            b.handle = None
+            b.pending = b.size
+
+    def zero_grad(self) -> None:
+        for b in self.buckets:
+            b.flat.zero_()
+            b.pending = b.size
+            b.handle = None
