@@ -32,6 +32,8 @@
 #include "dta_common.h"
 #include "dta_internal.h"
 
+#include <utility>
+
 namespace dta {
 
 // ------------------------------------------------------------ LDS images ---
@@ -81,6 +83,74 @@ struct Img {
     }
   }
 };
+
+// ---- compile-time loops (asm immediates must be constants, not unrolled loop indices)
+template <class F, int... I>
+__device__ __forceinline__ void sfor_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void sfor(F&& f) { sfor_impl(f, std::make_integer_sequence<int, N>{}); }
+
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)(p);
+}
+
+// 16-bit transposed operand reads, issued by inline asm: the builtin carries no
+// alias information, so the compiler guards every one of them with
+// s_waitcnt vmcnt(0) -- draining the LDS-DMA ring each tile.  Waits for these
+// reads are explicit (lgkm_pin).
+//
+// Addressing (derived from swz<ROWB>): for the 32-row block at row rbase and
+// columns 32d..32d+31, the byte address of lane l's piece of the k-step-s
+// fragment half x (x = 0: rows 16s+4h.., x = 1: rows 16s+8+4h..) is
+//     (Ltr(l) ^ (64 d + 32 x)) + ROWB * (rbase + 16 s + 8 x)
+// so one XOR per (d, x) and DS immediates carry the rest.
+template <int ROWB>
+__device__ __forceinline__ int tr_lane(int lane) {
+  const int h = (lane >> 5) & 1, i = lane & 15, q = i >> 2;
+  const int y = ((lane >> 4) & 1) * 2 + ((i & 3) >> 1);
+  int L = (4 * h + q) * ROWB + 16 * (y ^ h) + 8 * (i & 1);
+  if constexpr (ROWB >= 256) L += 64 * q;
+  else if constexpr (ROWB == 128) L += 64 * (q >> 1);
+  return L;
+}
+// operand row reads (ds_read_b128): row c32 of a 32-row block, k-step s:
+//     R*ROWB + (Lrow(l) ^ 32 s)
+template <int ROWB>
+__device__ __forceinline__ int row_lane(int lane) {
+  const int c = lane & 31, h = (lane >> 5) & 1;
+  return c * ROWB + 16 * (h ^ swz<ROWB>(c));
+}
+
+typedef long long lds64;
+// two fragments (k-steps s = 0, 1) of a 32x32 transposed operand block
+template <int ROWB, int RB>
+__device__ __forceinline__ void tr_issue(lds64 (&r)[4], unsigned a0, unsigned a1) {
+  asm volatile(
+      "ds_read_b64_tr_b16 %0, %4 offset:%6\n\t"
+      "ds_read_b64_tr_b16 %1, %5 offset:%7\n\t"
+      "ds_read_b64_tr_b16 %2, %4 offset:%8\n\t"
+      "ds_read_b64_tr_b16 %3, %5 offset:%9"
+      : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3])
+      : "v"(a0), "v"(a1), "i"(ROWB * RB), "i"(ROWB * (RB + 8)), "i"(ROWB * (RB + 16)), "i"(ROWB * (RB + 24)));
+}
+// retire every outstanding LDS read, then pin the asm results so no use of
+// them can be scheduled above the wait (cdna_hip_programming.md 5.7 item 1)
+template <int M>
+__device__ __forceinline__ void lgkm_pin(lds64 (&r)[M][4]) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int m = 0; m < M; ++m)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(r[m][j]));
+}
+template <class E>
+__device__ __forceinline__ typename Ops<E>::frag tr_frag(const lds64 (&r)[4], int s) {
+  typedef short v4s __attribute__((ext_vector_type(4)));
+  const v4s lo = __builtin_bit_cast(v4s, r[2 * s]), hi = __builtin_bit_cast(v4s, r[2 * s + 1]);
+  return __builtin_bit_cast(typename Ops<E>::frag, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
 
 // Stage ROWS x COLS elements (rows row0.., clamped to rowmax; only the first
 // VALID columns come from memory) into an image.  Whole-row 1 KiB pieces go by
@@ -133,7 +203,43 @@ __device__ __forceinline__ void stage_rows(float* dst, const float* src, int64_t
   }
 }
 
-__device__ __forceinline__ void wait_dma() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// LDS-DMA pieces one wave issues for a stage<> / stage_rows<> call (its j loop)
+template <int NI, int NW>
+__device__ __forceinline__ int pieces(int wave) { return NI / NW + (wave < NI % NW ? 1 : 0); }
+template <class E, int COLS, int ROWS, int VALID, int NW>
+__device__ __forceinline__ int stage_pieces(int wave) {
+  constexpr int BYTES = ROWS * Img<E, COLS>::ROWB;
+  if constexpr (VALID == COLS && BYTES % 1024 == 0) return pieces<BYTES / 1024, NW>(wave);
+  else return 0;                  // register path: its loads are retired by the LDS writes
+}
+template <int N, int NR, int NW>
+__device__ __forceinline__ int rows_pieces(int wave) { return pieces<(N * NR + 63) / 64, NW>(wave); }
+
+// s_waitcnt vmcnt(n) for a wave-uniform n.  Issued through the builtin (not
+// inline asm) so the compiler's wait-count tracking sees it.
+__device__ __forceinline__ void wait_vm(int n) {
+#define DTA_VM(k) case k: __builtin_amdgcn_s_waitcnt(((k) & 15) | (((k) >> 4) << 14) | (7 << 4) | (15 << 8)); break;
+  switch (n) {
+    DTA_VM(0) DTA_VM(1) DTA_VM(2) DTA_VM(3) DTA_VM(4) DTA_VM(5) DTA_VM(6) DTA_VM(7) DTA_VM(8) DTA_VM(9)
+    DTA_VM(10) DTA_VM(11) DTA_VM(12) DTA_VM(13) DTA_VM(14) DTA_VM(15) DTA_VM(16) DTA_VM(17) DTA_VM(18)
+    DTA_VM(19) DTA_VM(20) DTA_VM(21) DTA_VM(22) DTA_VM(23) DTA_VM(24) DTA_VM(25) DTA_VM(26) DTA_VM(27)
+    DTA_VM(28) DTA_VM(29) DTA_VM(30) DTA_VM(31)
+    default: __builtin_amdgcn_s_waitcnt(0 | (7 << 4) | (15 << 8));
+  }
+#undef DTA_VM
+}
+
+// Workgroup barrier that retires this wave's LDS reads but leaves LDS-DMA (vmcnt)
+// in flight -- __syncthreads() would drain every outstanding DMA.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_s_waitcnt(0xC07F);          // lgkmcnt(0) only
+  __builtin_amdgcn_s_barrier();
+}
+
+// Ring depth for a per-tile footprint: as many stages (2..4) as the LDS leaves room for.
+constexpr int ring_stages(int fixed_bytes, int tile_bytes) {
+  return (fixed_bytes + 4 * tile_bytes <= 160 * 1024) ? 4 : (fixed_bytes + 3 * tile_bytes <= 160 * 1024) ? 3 : 2;
+}
 
 // ---------------------------------------------------------------- forward ---
 template <class E> struct FwdTile { static constexpr int BN = 64; };
@@ -153,7 +259,8 @@ struct FwdCfg {
   static constexpr int nQ = QREG ? 0 : N * BM * HS;
   static constexpr int nK = N * BN * HS;
   static constexpr int nV = BN * DVC;
-  static constexpr int bytes = (nQ + 2 * nK + 2 * nV) * (int)sizeof(E);
+  static constexpr int NS = ring_stages(nQ * (int)sizeof(E), (nK + nV) * (int)sizeof(E));
+  static constexpr int bytes = (nQ + NS * nK + NS * nV) * (int)sizeof(E);
 };
 
 template <class E, int HS, int N>
@@ -187,10 +294,13 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_kernel(FwdParams p) {
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   E* Qs = reinterpret_cast<E*>(smem);
-  E* Kb = Qs + CF::nQ;              // [2][N][BN][HS]
-  E* Vb = Kb + 2 * CF::nK;          // [2][BN][DVC]
+  constexpr int NS = CF::NS;
+  E* Kb = Qs + CF::nQ;              // [NS][N][BN][HS]  ring
+  E* Vb = Kb + NS * CF::nK;         // [NS][BN][DVC]
 
-  const int wave = threadIdx.x >> 6;
+  // wave index is wave-uniform: make it provably so (SGPR), or every branch on it
+  // becomes an exec-masked divergent branch
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int tid = threadIdx.x, lane = tid & 63;
   int hf = lane >> 5, c32 = lane & 31;
   const int nblk = gridDim.x * gridDim.y * gridDim.z;
@@ -234,9 +344,11 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_kernel(FwdParams p) {
       stage<E, HS, BN, HS, NTHR>(Kb + (buf * N + i) * BN * HS, gk + i * p.k.si, p.k.st, k0, T - 1, tid);
     stage<E, DVC, BN, DVC, NTHR>(Vb + buf * BN * DVC, gv, p.v.st, k0, T - 1, tid);
   };
-  stage_kv(0, 0);
-  wait_dma();
-  __syncthreads();
+  const int tile_pieces = N * stage_pieces<E, HS, BN, HS, NW>(wave) + stage_pieces<E, DVC, BN, DVC, NW>(wave);
+  for (int j = 0; j < NS - 1; ++j)
+    if (j < ntiles) stage_kv(j, j);
+  wait_vm(tile_pieces * max(0, min(NS - 1, ntiles) - 1));   // tile 0 (and the Q block) landed
+  lds_barrier();
 
   f32x16 acc[N][NDB];
   float m[N], l[N];
@@ -255,8 +367,8 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_kernel(FwdParams p) {
     asm volatile("" : "+v"(lane));
     tid = (wave << 6) + lane; hf = lane >> 5; c32 = lane & 31;
     qrow = qw0 + c32;
-    const int buf = kt & 1;
-    if (kt + 1 < ntiles) stage_kv(kt + 1, buf ^ 1);
+    const int buf = kt % NS;
+    if (kt + NS - 1 < ntiles) stage_kv(kt + NS - 1, (kt + NS - 1) % NS);
     const int k0 = kt * BN;
     if (wave_live && k0 <= qw0 + 31) {
       const E* Kc = Kb + buf * N * BN * HS;
@@ -324,19 +436,40 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_kernel(FwdParams p) {
         }
       }
       // O_i^T += V^T P_i^T, one V fragment feeds every branch
+      if constexpr (sizeof(E) == 2) {
+        const unsigned vb = lds_addr(Vc);
+        const int Lv = tr_lane<VI::ROWB>(lane);
+        sfor<NDB>([&](auto D) {
+          constexpr int d = decltype(D)::value;
+          lds64 r[NKB][4];
+          const unsigned a0 = vb + (Lv ^ (64 * d)), a1 = vb + (Lv ^ (64 * d + 32));
+          sfor<NKB>([&](auto KB) { tr_issue<VI::ROWB, 32 * decltype(KB)::value>(r[decltype(KB)::value], a0, a1); });
+          lgkm_pin<NKB>(r);
 #pragma unroll
-      for (int d = 0; d < NDB; ++d)
+          for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
-        for (int kb = 0; kb < NKB; ++kb)
+            for (int s = 0; s < 2; ++s) {
+              const frag va = tr_frag<E>(r[kb], s);
 #pragma unroll
-          for (int s = 0; s < SPB; ++s) {
-            const frag va = VI::tr_perm(Vc, kb * 32, s, hf, d * 32, lane);
+              for (int i = 0; i < N; ++i) acc[i][d] = O::mma(va, pf[i][kb * 2 + s], acc[i][d]);
+            }
+        });
+      } else {
 #pragma unroll
-            for (int i = 0; i < N; ++i) acc[i][d] = O::mma(va, pf[i][kb * SPB + s], acc[i][d]);
-          }
+        for (int d = 0; d < NDB; ++d)
+#pragma unroll
+          for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+            for (int s = 0; s < SPB; ++s) {
+              const frag va = VI::tr_perm(Vc, kb * 32, s, hf, d * 32, lane);
+#pragma unroll
+              for (int i = 0; i < N; ++i) acc[i][d] = O::mma(va, pf[i][kb * SPB + s], acc[i][d]);
+            }
+      }
     }
-    wait_dma();
-    __syncthreads();
+    // tile kt+1 must have landed; younger tiles may stay in flight
+    wait_vm(tile_pieces * max(0, min(NS - 2, ntiles - 2 - kt)));
+    lds_barrier();
   }
 
   if (!wave_live || qrow >= T) return;
@@ -377,7 +510,8 @@ struct DqCfg {
   static constexpr int nQ = QREG ? 0 : N * BM * HS;
   static constexpr int nK = N * BN * HSP;
   static constexpr int nV = BN * DV;
-  static constexpr int bytes = (nQ + 2 * nK + 2 * nV) * (int)sizeof(E);
+  static constexpr int NS = ring_stages(nQ * (int)sizeof(E), (nK + nV) * (int)sizeof(E));
+  static constexpr int bytes = (nQ + NS * nK + NS * nV) * (int)sizeof(E);
 };
 
 template <class E, int HS, int N>
@@ -405,10 +539,13 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_dq_kernel(BwdParams p) {
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   E* Qs = reinterpret_cast<E*>(smem);   // [N][BM][HS] unless QREG
-  E* Kb = Qs + CF::nQ;                  // [2][N][BN][HSP]
-  E* Vb = Kb + 2 * CF::nK;              // [2][BN][DV]
+  constexpr int NS = CF::NS;
+  E* Kb = Qs + CF::nQ;                  // [NS][N][BN][HSP]  ring
+  E* Vb = Kb + NS * CF::nK;             // [NS][BN][DV]
 
-  const int wave = threadIdx.x >> 6;
+  // wave index is wave-uniform: make it provably so (SGPR), or every branch on it
+  // becomes an exec-masked divergent branch
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int tid = threadIdx.x, lane = tid & 63;
   int hf = lane >> 5, c32 = lane & 31;
   const int nblk = gridDim.x * gridDim.y * gridDim.z;
@@ -483,9 +620,11 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_dq_kernel(BwdParams p) {
 #pragma unroll
     for (int i = 0; i < N; ++i) stage<E, HS, BM, HS, NTHR>(Qs + i * BM * HS, gq + i * p.q.si, p.q.st, q0, T - 1, tid);
   }
-  stage_kv(0, 0);
-  wait_dma();
-  __syncthreads();
+  const int tile_pieces = N * stage_pieces<E, HSP, BN, HS, NW>(wave) + stage_pieces<E, DV, BN, DV, NW>(wave);
+  for (int j = 0; j < NS - 1; ++j)
+    if (j < ntiles) stage_kv(j, j);
+  wait_vm(tile_pieces * max(0, min(NS - 1, ntiles) - 1));
+  lds_barrier();
 
   f32x16 dq[N][NHB];
 #pragma unroll
@@ -500,8 +639,8 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_dq_kernel(BwdParams p) {
     asm volatile("" : "+v"(lane));
     tid = (wave << 6) + lane; hf = lane >> 5; c32 = lane & 31;
     qrow = qw0 + c32;
-    const int buf = kt & 1;
-    if (kt + 1 < ntiles) stage_kv(kt + 1, buf ^ 1);
+    const int buf = kt % NS;
+    if (kt + NS - 1 < ntiles) stage_kv(kt + NS - 1, (kt + NS - 1) % NS);
     const int k0 = kt * BN;
     if (wave_live && k0 <= qw0 + 31) {
       const E* Kc = Kb + buf * N * BN * HSP;
@@ -542,23 +681,34 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_dq_kernel(BwdParams p) {
             sa[kb][r] = ci * pr * (dp[kb][r] - di);
           }
         // dQ_i^T += K_i^T dS_i^T
+        if constexpr (sizeof(E) == 2) {
+          const unsigned kbse = lds_addr(Ki);
+          const int Lk = tr_lane<KI::ROWB>(lane);
+          sfor<NHB>([&](auto D) {
+            constexpr int d = decltype(D)::value;
+            lds64 r[NKB][4];
+            const unsigned a0 = kbse + (Lk ^ (64 * d)), a1 = kbse + (Lk ^ (64 * d + 32));
+            sfor<NKB>([&](auto KB) { tr_issue<KI::ROWB, 32 * decltype(KB)::value>(r[decltype(KB)::value], a0, a1); });
+            lgkm_pin<NKB>(r);
 #pragma unroll
-        for (int d = 0; d < NHB; ++d)
+            for (int kb = 0; kb < NKB; ++kb) {
+              dq[i][d] = O::mma(tr_frag<E>(r[kb], 0), O::template pack<0>(sa[kb]), dq[i][d]);
+              dq[i][d] = O::mma(tr_frag<E>(r[kb], 1), O::template pack<1>(sa[kb]), dq[i][d]);
+            }
+          });
+        } else {
 #pragma unroll
-          for (int kb = 0; kb < NKB; ++kb) {
-            if constexpr (SPB == 2) {
-              dq[i][d] = O::mma(KI::tr_perm(Ki, kb * 32, 0, hf, d * 32, lane), O::template pack<0>(sa[kb]), dq[i][d]);
-              dq[i][d] = O::mma(KI::tr_perm(Ki, kb * 32, 1, hf, d * 32, lane), O::template pack<1>(sa[kb]), dq[i][d]);
-            } else {
+          for (int d = 0; d < NHB; ++d)
+#pragma unroll
+            for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
               for (int s = 0; s < SPB; ++s)
                 dq[i][d] = O::mma(KI::tr_perm(Ki, kb * 32, s, hf, d * 32, lane), sa[kb][s], dq[i][d]);
-            }
-          }
+        }
       }
     }
-    wait_dma();
-    __syncthreads();
+    wait_vm(tile_pieces * max(0, min(NS - 2, ntiles - 2 - kt)));
+    lds_barrier();
   }
 
   if (!rowok) return;
@@ -594,7 +744,8 @@ struct DkdvCfg {
   static constexpr int nQ = N * BQ * HSP;
   static constexpr int nD = BQ * DV;
   static constexpr int nK = N * BK * HS;                   // the workgroup's K_i rows (B of S_i)
-  static constexpr int bytes = (nK + 2 * nQ + 2 * nD) * (int)sizeof(E) + 2 * 2 * NP * 4;
+  static constexpr int NS = ring_stages(nK * (int)sizeof(E), (nQ + nD) * (int)sizeof(E) + 2 * NP * 4);
+  static constexpr int bytes = (nK + NS * nQ + NS * nD) * (int)sizeof(E) + NS * 2 * NP * 4;
 };
 
 // accumulator budget -> whether dK and dV share one launch
@@ -620,11 +771,14 @@ __global__ __launch_bounds__(NW * 64, (NW >= 8 ? 2 : 1)) void attn_dkdv_kernel(B
   extern __shared__ __attribute__((aligned(16))) char smem[];
   E* Ks = reinterpret_cast<E*>(smem);     // [N][BK][HS]
   E* Qb = Ks + CF::nK;                    // [2][N][BQ][HSP]
-  E* Db = Qb + 2 * CF::nQ;                // [2][BQ][DV]
-  float* Lb = reinterpret_cast<float*>(Db + 2 * CF::nD);   // [2][NP] lse
-  float* Gb = Lb + 2 * NP;                                  // [2][NP] delta
+  constexpr int NS = CF::NS;
+  E* Db = Qb + NS * CF::nQ;               // [NS][BQ][DV]
+  float* Lb = reinterpret_cast<float*>(Db + NS * CF::nD);  // [NS][NP] lse
+  float* Gb = Lb + NS * NP;                                 // [NS][NP] delta
 
-  const int wave = threadIdx.x >> 6;
+  // wave index is wave-uniform: make it provably so (SGPR), or every branch on it
+  // becomes an exec-masked divergent branch
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int tid = threadIdx.x, lane = tid & 63;
   int hf = lane >> 5, c32 = lane & 31;
   const int nblk = gridDim.x * gridDim.y * gridDim.z;
@@ -676,9 +830,12 @@ __global__ __launch_bounds__(NW * 64, (NW >= 8 ? 2 : 1)) void attn_dkdv_kernel(B
   const int ntiles = kb0 < T ? (T - kb0 + BQ - 1) / BQ : 0;
 #pragma unroll
   for (int i = 0; i < N; ++i) stage<E, HS, BK, HS, NTHR>(Ks + i * BK * HS, gk + i * p.k.si, p.k.st, kb0, T - 1, tid);
-  if (ntiles > 0) stage_q(kb0, 0);
-  wait_dma();
-  __syncthreads();
+  const int tile_pieces = N * stage_pieces<E, HSP, BQ, HS, NW>(wave) + stage_pieces<E, DV, BQ, DV, NW>(wave) +
+                          rows_pieces<N, BQ, NW>(wave) * (DK ? 2 : 1);
+  for (int j = 0; j < NS - 1; ++j)
+    if (j < ntiles) stage_q(kb0 + j * BQ, j);
+  wait_vm(tile_pieces * max(0, min(NS - 1, ntiles) - 1));
+  lds_barrier();
   const bool wave_keys = kw0 < T;
 
   for (int t = 0; t < ntiles; ++t) {
@@ -687,9 +844,9 @@ __global__ __launch_bounds__(NW * 64, (NW >= 8 ? 2 : 1)) void attn_dkdv_kernel(B
     asm volatile("" : "+v"(lane));
     tid = (wave << 6) + lane; hf = lane >> 5; c32 = lane & 31;
     krow = kw0 + c32;
-    const int buf = t & 1;
+    const int buf = t % NS;
     const int q0 = kb0 + t * BQ;
-    if (t + 1 < ntiles) stage_q(q0 + BQ, buf ^ 1);
+    if (t + NS - 1 < ntiles) stage_q(q0 + (NS - 1) * BQ, (t + NS - 1) % NS);
     if (wave_keys && q0 + BQ - 1 >= kw0) {
       const E* Qc = Qb + buf * N * BQ * HSP;
       const E* Dc = Db + buf * BQ * DV;
@@ -728,33 +885,59 @@ __global__ __launch_bounds__(NW * 64, (NW >= 8 ? 2 : 1)) void attn_dkdv_kernel(B
           }
         }
         if constexpr (DK) {
+          if constexpr (sizeof(E) == 2) {
+            const unsigned qb = lds_addr(Qi);
+            const int Lq = tr_lane<QI::ROWB>(lane);
+            lds64 r[NHB][4];
+            sfor<NHB>([&](auto D) {
+              constexpr int d = decltype(D)::value;
+              tr_issue<QI::ROWB, 0>(r[d], qb + (Lq ^ (64 * d)), qb + (Lq ^ (64 * d + 32)));
+            });
+            lgkm_pin<NHB>(r);
+            const frag p0 = O::template pack<0>(sa), p1 = O::template pack<1>(sa);
 #pragma unroll
-          for (int d = 0; d < NHB; ++d) {
-            if constexpr (SPB == 2) {
-              dk[i][d] = O::mma(QI::tr_perm(Qi, 0, 0, hf, d * 32, lane), O::template pack<0>(sa), dk[i][d]);
-              dk[i][d] = O::mma(QI::tr_perm(Qi, 0, 1, hf, d * 32, lane), O::template pack<1>(sa), dk[i][d]);
-            } else {
+            for (int d = 0; d < NHB; ++d) {
+              dk[i][d] = O::mma(tr_frag<E>(r[d], 0), p0, dk[i][d]);
+              dk[i][d] = O::mma(tr_frag<E>(r[d], 1), p1, dk[i][d]);
+            }
+          } else {
+#pragma unroll
+            for (int d = 0; d < NHB; ++d)
 #pragma unroll
               for (int s = 0; s < SPB; ++s) dk[i][d] = O::mma(QI::tr_perm(Qi, 0, s, hf, d * 32, lane), sa[s], dk[i][d]);
-            }
           }
         }
       }
       if constexpr (DVV) {
+        if constexpr (sizeof(E) == 2) {
+          const unsigned db = lds_addr(Dc);
+          const int Ld = tr_lane<DI::ROWB>(lane);
+          const frag p0 = O::template pack<0>(pc), p1 = O::template pack<1>(pc);
+          constexpr int NP2 = NVB >= 2 ? 2 : 1;       // d-blocks per LDS read batch
+          sfor<NVB / NP2>([&](auto D2) {
+            constexpr int d0 = NP2 * decltype(D2)::value;
+            lds64 r[NP2][4];
+            sfor<NP2>([&](auto E2) {
+              constexpr int d = d0 + decltype(E2)::value;
+              tr_issue<DI::ROWB, 0>(r[decltype(E2)::value], db + (Ld ^ (64 * d)), db + (Ld ^ (64 * d + 32)));
+            });
+            lgkm_pin<NP2>(r);
 #pragma unroll
-        for (int d = 0; d < NVB; ++d) {
-          if constexpr (SPB == 2) {
-            dv[d] = O::mma(DI::tr_perm(Dc, 0, 0, hf, d * 32, lane), O::template pack<0>(pc), dv[d]);
-            dv[d] = O::mma(DI::tr_perm(Dc, 0, 1, hf, d * 32, lane), O::template pack<1>(pc), dv[d]);
-          } else {
+            for (int e = 0; e < NP2; ++e) {
+              dv[d0 + e] = O::mma(tr_frag<E>(r[e], 0), p0, dv[d0 + e]);
+              dv[d0 + e] = O::mma(tr_frag<E>(r[e], 1), p1, dv[d0 + e]);
+            }
+          });
+        } else {
+#pragma unroll
+          for (int d = 0; d < NVB; ++d)
 #pragma unroll
             for (int s = 0; s < SPB; ++s) dv[d] = O::mma(DI::tr_perm(Dc, 0, s, hf, d * 32, lane), pc[s], dv[d]);
-          }
         }
       }
     }
-    wait_dma();
-    __syncthreads();
+    wait_vm(tile_pieces * max(0, min(NS - 2, ntiles - 2 - t)));
+    lds_barrier();
   }
 
   if (!wave_keys || krow >= T) return;
