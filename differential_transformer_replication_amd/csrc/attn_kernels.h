@@ -361,7 +361,11 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_kernel(FwdParams p) {
   }
   const bool wave_live = qw0 < T;
 
-  for (int kt = 0; kt < ntiles; ++kt) {
+  // two loops over straight-line bodies: tiles strictly below the block's first
+  // query row and inside T need no mask; the block's diagonal / tail tiles do
+  // (one loop body with both variants behind a branch spills)
+  auto step = [&](int kt, auto MASKED) {
+    constexpr bool MASK = decltype(MASKED)::value;
     // keep lane-derived addresses loop-variant: recomputed per tile instead of
     // hoisted into (spilled) registers across the whole loop
     asm volatile("" : "+v"(lane));
@@ -373,104 +377,127 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_kernel(FwdParams p) {
     if (wave_live && k0 <= qw0 + 31) {
       const E* Kc = Kb + buf * N * BN * HS;
       const E* Vc = Vb + buf * BN * DVC;
-      const bool needmask = (k0 + BN - 1 > qw0) || (k0 + BN > T);
-      frag pf[N][NKB * SPB];
+      {
+        frag pf[N][NKB * SPB];
 #pragma unroll
-      for (int i = 0; i < N; ++i) {
-        f32x16 sa[NKB];
-        const E* Ki = Kc + i * BN * HS;
+        for (int i = 0; i < N; ++i) {
+          f32x16 sa[NKB];
+          const E* Ki = Kc + i * BN * HS;
+          if constexpr (sizeof(E) == 2) {
+            // row operands: byte R*ROWB + (Lrow ^ 32 s) for a 32-row block at row R
+            const int Lr = row_lane<KI::ROWB>(lane);
+            const char* kbase = reinterpret_cast<const char*>(Ki);
+            const char* qbase = reinterpret_cast<const char*>(Qs + i * BM * HS) + wave * 32 * QI::ROWB;
 #pragma unroll
-        for (int kb = 0; kb < NKB; ++kb) {
-          sa[kb] = f32x16{};
+            for (int kb = 0; kb < NKB; ++kb) sa[kb] = f32x16{};
 #pragma unroll
-          for (int s = 0; s < NSQ; ++s) {
-            frag qb;
-            if constexpr (QREG) qb = qf[i][s];
-            else qb = QI::row(Qs + i * BM * HS, wave * 32 + c32, s, hf);
-            sa[kb] = O::mma(KI::row(Ki, kb * 32 + c32, s, hf), qb, sa[kb]);
+            for (int s = 0; s < NSQ; ++s) {
+              const int o = Lr ^ (32 * s);
+              frag qb;
+              if constexpr (QREG) qb = qf[i][s];
+              else qb = *reinterpret_cast<const frag*>(qbase + o);
+#pragma unroll
+              for (int kb = 0; kb < NKB; ++kb)
+                sa[kb] = O::mma(*reinterpret_cast<const frag*>(kbase + kb * 32 * KI::ROWB + o), qb, sa[kb]);
+            }
+          } else {
+#pragma unroll
+            for (int kb = 0; kb < NKB; ++kb) {
+              sa[kb] = f32x16{};
+#pragma unroll
+              for (int s = 0; s < NSQ; ++s) {
+                frag qb;
+                if constexpr (QREG) qb = qf[i][s];
+                else qb = QI::row(Qs + i * BM * HS, wave * 32 + c32, s, hf);
+                sa[kb] = O::mma(KI::row(Ki, kb * 32 + c32, s, hf), qb, sa[kb]);
+              }
+            }
           }
-        }
-        if (needmask) {
+          if constexpr (MASK) {
+            // key = k0 + kb*32 + rowof(r); masked when key > qrow or key >= T
+            const int lim = min(qrow, T - 1) - k0 - 4 * hf;
+#pragma unroll
+            for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+              for (int r = 0; r < 16; ++r)
+                sa[kb][r] = (kb * 32 + (r & 3) + 8 * (r >> 2) > lim) ? -INFINITY : sa[kb][r];
+          }
+          float mx = -INFINITY;
+#pragma unroll
+          for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+            for (int r = 0; r < 16; r += 2) mx = fmaxf(mx, fmaxf(sa[kb][r], sa[kb][r + 1]));
+          mx = wave_max_halves(mx) * p.sl2;
+          if (__any(mx > m[i] + THR)) {          // rescale only when some row's max grew by > 2^THR
+            const float mnew = fmaxf(m[i], mx);
+            const float alpha = exp2_fast(m[i] - mnew);
+            m[i] = mnew;
+            l[i] *= alpha;
+#pragma unroll
+            for (int d = 0; d < NDB; ++d) acc[i][d] *= alpha;
+          }
+          const float mi = m[i];
+          float ls = 0.f;
 #pragma unroll
           for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-              const int key = k0 + kb * 32 + rowof(r, hf);
-              if (key > qrow || key >= T) sa[kb][r] = -INFINITY;
+              const float e = exp2_fast(fmaf(sa[kb][r], p.sl2, -mi));
+              sa[kb][r] = e;
+              ls += e;
             }
-        }
-        float mx = -INFINITY;
+          l[i] += ls;
 #pragma unroll
-        for (int kb = 0; kb < NKB; ++kb)
+          for (int kb = 0; kb < NKB; ++kb) {
+            if constexpr (SPB == 2) {
+              pf[i][kb * 2 + 0] = O::template pack<0>(sa[kb]);
+              pf[i][kb * 2 + 1] = O::template pack<1>(sa[kb]);
+            } else {
 #pragma unroll
-          for (int r = 0; r < 16; r += 2) mx = fmaxf(mx, fmaxf(sa[kb][r], sa[kb][r + 1]));
-        mx = wave_max_halves(mx) * p.sl2;
-        if (__any(mx > m[i] + THR)) {          // rescale only when some row's max grew by > 2^THR
-          const float mnew = fmaxf(m[i], mx);
-          const float alpha = exp2_fast(m[i] - mnew);
-          m[i] = mnew;
-          l[i] *= alpha;
-#pragma unroll
-          for (int d = 0; d < NDB; ++d) acc[i][d] *= alpha;
-        }
-        const float mi = m[i];
-        float ls = 0.f;
-#pragma unroll
-        for (int kb = 0; kb < NKB; ++kb)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const float e = exp2_fast(fmaf(sa[kb][r], p.sl2, -mi));
-            sa[kb][r] = e;
-            ls += e;
-          }
-        l[i] += ls;
-#pragma unroll
-        for (int kb = 0; kb < NKB; ++kb) {
-          if constexpr (SPB == 2) {
-            pf[i][kb * 2 + 0] = O::template pack<0>(sa[kb]);
-            pf[i][kb * 2 + 1] = O::template pack<1>(sa[kb]);
-          } else {
-#pragma unroll
-            for (int s = 0; s < 16; ++s) pf[i][kb * SPB + s] = sa[kb][s];
+              for (int s = 0; s < 16; ++s) pf[i][kb * SPB + s] = sa[kb][s];
+            }
           }
         }
-      }
-      // O_i^T += V^T P_i^T, one V fragment feeds every branch
-      if constexpr (sizeof(E) == 2) {
-        const unsigned vb = lds_addr(Vc);
-        const int Lv = tr_lane<VI::ROWB>(lane);
-        sfor<NDB>([&](auto D) {
-          constexpr int d = decltype(D)::value;
-          lds64 r[NKB][4];
-          const unsigned a0 = vb + (Lv ^ (64 * d)), a1 = vb + (Lv ^ (64 * d + 32));
-          sfor<NKB>([&](auto KB) { tr_issue<VI::ROWB, 32 * decltype(KB)::value>(r[decltype(KB)::value], a0, a1); });
-          lgkm_pin<NKB>(r);
+        // O_i^T += V^T P_i^T, one V fragment feeds every branch
+        if constexpr (sizeof(E) == 2) {
+          const unsigned vb = lds_addr(Vc);
+          const int Lv = tr_lane<VI::ROWB>(lane);
+          sfor<NDB>([&](auto D) {
+            constexpr int d = decltype(D)::value;
+            lds64 r[NKB][4];
+            const unsigned a0 = vb + (Lv ^ (64 * d)), a1 = vb + (Lv ^ (64 * d + 32));
+            sfor<NKB>([&](auto KB) { tr_issue<VI::ROWB, 32 * decltype(KB)::value>(r[decltype(KB)::value], a0, a1); });
+            lgkm_pin<NKB>(r);
 #pragma unroll
-          for (int kb = 0; kb < NKB; ++kb)
+            for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
-            for (int s = 0; s < 2; ++s) {
-              const frag va = tr_frag<E>(r[kb], s);
+              for (int s = 0; s < 2; ++s) {
+                const frag va = tr_frag<E>(r[kb], s);
 #pragma unroll
-              for (int i = 0; i < N; ++i) acc[i][d] = O::mma(va, pf[i][kb * 2 + s], acc[i][d]);
-            }
-        });
-      } else {
+                for (int i = 0; i < N; ++i) acc[i][d] = O::mma(va, pf[i][kb * 2 + s], acc[i][d]);
+              }
+          });
+        } else {
 #pragma unroll
-        for (int d = 0; d < NDB; ++d)
+          for (int d = 0; d < NDB; ++d)
 #pragma unroll
-          for (int kb = 0; kb < NKB; ++kb)
+            for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
-            for (int s = 0; s < SPB; ++s) {
-              const frag va = VI::tr_perm(Vc, kb * 32, s, hf, d * 32, lane);
+              for (int s = 0; s < SPB; ++s) {
+                const frag va = VI::tr_perm(Vc, kb * 32, s, hf, d * 32, lane);
 #pragma unroll
-              for (int i = 0; i < N; ++i) acc[i][d] = O::mma(va, pf[i][kb * SPB + s], acc[i][d]);
-            }
+                for (int i = 0; i < N; ++i) acc[i][d] = O::mma(va, pf[i][kb * SPB + s], acc[i][d]);
+              }
+        }
       }
     }
     // tile kt+1 must have landed; younger tiles may stay in flight
     wait_vm(tile_pieces * max(0, min(NS - 2, ntiles - 2 - kt)));
     lds_barrier();
-  }
+  };
+  const int nfull = min(ntiles, min((q0 + 1) / BN, T / BN));
+  for (int kt = 0; kt < nfull; ++kt) step(kt, std::false_type{});
+  for (int kt = nfull; kt < ntiles; ++kt) step(kt, std::true_type{});
 
   if (!wave_live || qrow >= T) return;
   float inv[N];
@@ -608,7 +635,7 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_dq_kernel(BwdParams p) {
     }
     d = wave_sum_halves(d);
     del[i] = d;
-    if (rowok && hf == 0) p.delta[rs + i * bstride] = d;
+    if (rowok && hf == 0) p.delta[rs + i * bstride] = coef[i] * d;     // c_i * delta_i for attn_dkdv
     // d(coef)[h][i] = sum over rows of delta_i: one atomic per wave
     float w = (rowok && hf == 0) ? d : 0.f;
 #pragma unroll
@@ -633,7 +660,9 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_dq_kernel(BwdParams p) {
     for (int d = 0; d < NHB; ++d) dq[i][d] = f32x16{};
   const bool wave_live = qw0 < T;
 
-  for (int kt = 0; kt < ntiles; ++kt) {
+  // unmasked loop, then the block's diagonal / tail tiles (see attn_fwd_kernel)
+  auto step = [&](int kt, auto MASKED) {
+    constexpr bool MASK = decltype(MASKED)::value;
     // keep lane-derived addresses loop-variant: recomputed per tile instead of
     // hoisted into (spilled) registers across the whole loop
     asm volatile("" : "+v"(lane));
@@ -645,71 +674,106 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_dq_kernel(BwdParams p) {
     if (wave_live && k0 <= qw0 + 31) {
       const E* Kc = Kb + buf * N * BN * HSP;
       const E* Vc = Vb + buf * BN * DV;
-      const bool needmask = (k0 + BN - 1 > qw0) || (k0 + BN > T);
-      f32x16 dp[NKB];
-#pragma unroll
-      for (int kb = 0; kb < NKB; ++kb) {
-        dp[kb] = f32x16{};
-#pragma unroll
-        for (int s = 0; s < NSV; ++s) dp[kb] = O::mma(VI::row(Vc, kb * 32 + c32, s, hf), df[s], dp[kb]);
-      }
-#pragma unroll
-      for (int i = 0; i < N; ++i) {
-        const E* Ki = Kc + i * BN * HSP;
-        f32x16 sa[NKB];
-#pragma unroll
-        for (int kb = 0; kb < NKB; ++kb) {
-          sa[kb] = f32x16{};
-#pragma unroll
-          for (int s = 0; s < NSQ; ++s) {
-            frag qb;
-            if constexpr (QREG) qb = qf[i][s];
-            else qb = QI::row(Qs + i * BM * HS, wave * 32 + c32, s, hf);
-            sa[kb] = O::mma(KI::row(Ki, kb * 32 + c32, s, hf), qb, sa[kb]);
-          }
-        }
-        const float li = lse[i], di = del[i], ci = coef[i];
-#pragma unroll
-        for (int kb = 0; kb < NKB; ++kb)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            float pr = exp2_fast(fmaf(sa[kb][r], p.sl2, -li));
-            if (needmask) {
-              const int key = k0 + kb * 32 + rowof(r, hf);
-              if (key > qrow || key >= T) pr = 0.f;
-            }
-            sa[kb][r] = ci * pr * (dp[kb][r] - di);
-          }
-        // dQ_i^T += K_i^T dS_i^T
+      {
+        f32x16 dp[NKB];
         if constexpr (sizeof(E) == 2) {
-          const unsigned kbse = lds_addr(Ki);
-          const int Lk = tr_lane<KI::ROWB>(lane);
-          sfor<NHB>([&](auto D) {
-            constexpr int d = decltype(D)::value;
-            lds64 r[NKB][4];
-            const unsigned a0 = kbse + (Lk ^ (64 * d)), a1 = kbse + (Lk ^ (64 * d + 32));
-            sfor<NKB>([&](auto KB) { tr_issue<KI::ROWB, 32 * decltype(KB)::value>(r[decltype(KB)::value], a0, a1); });
-            lgkm_pin<NKB>(r);
+          const int Lv = row_lane<VI::ROWB>(lane);
+          const char* vbase = reinterpret_cast<const char*>(Vc);
 #pragma unroll
-            for (int kb = 0; kb < NKB; ++kb) {
-              dq[i][d] = O::mma(tr_frag<E>(r[kb], 0), O::template pack<0>(sa[kb]), dq[i][d]);
-              dq[i][d] = O::mma(tr_frag<E>(r[kb], 1), O::template pack<1>(sa[kb]), dq[i][d]);
-            }
-          });
-        } else {
+          for (int kb = 0; kb < NKB; ++kb) dp[kb] = f32x16{};
 #pragma unroll
-          for (int d = 0; d < NHB; ++d)
+          for (int s = 0; s < NSV; ++s) {
+            const int o = Lv ^ (32 * s);
 #pragma unroll
             for (int kb = 0; kb < NKB; ++kb)
+              dp[kb] = O::mma(*reinterpret_cast<const frag*>(vbase + kb * 32 * VI::ROWB + o), df[s], dp[kb]);
+          }
+        } else {
 #pragma unroll
-              for (int s = 0; s < SPB; ++s)
-                dq[i][d] = O::mma(KI::tr_perm(Ki, kb * 32, s, hf, d * 32, lane), sa[kb][s], dq[i][d]);
+          for (int kb = 0; kb < NKB; ++kb) {
+            dp[kb] = f32x16{};
+#pragma unroll
+            for (int s = 0; s < NSV; ++s) dp[kb] = O::mma(VI::row(Vc, kb * 32 + c32, s, hf), df[s], dp[kb]);
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+          const E* Ki = Kc + i * BN * HSP;
+          f32x16 sa[NKB];
+          if constexpr (sizeof(E) == 2) {
+            const int Lr = row_lane<KI::ROWB>(lane);
+            const char* kbase = reinterpret_cast<const char*>(Ki);
+            const char* qbase = reinterpret_cast<const char*>(Qs + i * BM * HS) + wave * 32 * QI::ROWB;
+            const int Lq = row_lane<QI::ROWB>(lane);
+#pragma unroll
+            for (int kb = 0; kb < NKB; ++kb) sa[kb] = f32x16{};
+#pragma unroll
+            for (int s = 0; s < NSQ; ++s) {
+              frag qb;
+              if constexpr (QREG) qb = qf[i][s];
+              else qb = *reinterpret_cast<const frag*>(qbase + (Lq ^ (32 * s)));
+#pragma unroll
+              for (int kb = 0; kb < NKB; ++kb)
+                sa[kb] = O::mma(*reinterpret_cast<const frag*>(kbase + kb * 32 * KI::ROWB + (Lr ^ (32 * s))), qb, sa[kb]);
+            }
+          } else {
+#pragma unroll
+            for (int kb = 0; kb < NKB; ++kb) {
+              sa[kb] = f32x16{};
+#pragma unroll
+              for (int s = 0; s < NSQ; ++s) {
+                frag qb;
+                if constexpr (QREG) qb = qf[i][s];
+                else qb = QI::row(Qs + i * BM * HS, wave * 32 + c32, s, hf);
+                sa[kb] = O::mma(KI::row(Ki, kb * 32 + c32, s, hf), qb, sa[kb]);
+              }
+            }
+          }
+          // dS^T = c_i P^T (dP^T - delta_i) = P^T * (c_i dP^T - c_i delta_i)
+          const float li = lse[i], ci = coef[i], cdi = coef[i] * del[i];
+          const int lim = min(qrow, T - 1) - k0 - 4 * hf;
+#pragma unroll
+          for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              float arg = fmaf(sa[kb][r], p.sl2, -li);
+              if constexpr (MASK) arg = (kb * 32 + (r & 3) + 8 * (r >> 2) > lim) ? -INFINITY : arg;
+              sa[kb][r] = exp2_fast(arg) * fmaf(ci, dp[kb][r], -cdi);
+            }
+          // dQ_i^T += K_i^T dS_i^T
+          if constexpr (sizeof(E) == 2) {
+            const unsigned kbse = lds_addr(Ki);
+            const int Lk = tr_lane<KI::ROWB>(lane);
+            sfor<NHB>([&](auto D) {
+              constexpr int d = decltype(D)::value;
+              lds64 r[NKB][4];
+              const unsigned a0 = kbse + (Lk ^ (64 * d)), a1 = kbse + (Lk ^ (64 * d + 32));
+              sfor<NKB>([&](auto KB) { tr_issue<KI::ROWB, 32 * decltype(KB)::value>(r[decltype(KB)::value], a0, a1); });
+              lgkm_pin<NKB>(r);
+#pragma unroll
+              for (int kb = 0; kb < NKB; ++kb) {
+                dq[i][d] = O::mma(tr_frag<E>(r[kb], 0), O::template pack<0>(sa[kb]), dq[i][d]);
+                dq[i][d] = O::mma(tr_frag<E>(r[kb], 1), O::template pack<1>(sa[kb]), dq[i][d]);
+              }
+            });
+          } else {
+#pragma unroll
+            for (int d = 0; d < NHB; ++d)
+#pragma unroll
+              for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+                for (int s = 0; s < SPB; ++s)
+                  dq[i][d] = O::mma(KI::tr_perm(Ki, kb * 32, s, hf, d * 32, lane), sa[kb][s], dq[i][d]);
+          }
         }
       }
     }
     wait_vm(tile_pieces * max(0, min(NS - 2, ntiles - 2 - kt)));
     lds_barrier();
-  }
+  };
+  const int nfull = min(ntiles, min((q0 + 1) / BN, T / BN));
+  for (int kt = 0; kt < nfull; ++kt) step(kt, std::false_type{});
+  for (int kt = nfull; kt < ntiles; ++kt) step(kt, std::true_type{});
 
   if (!rowok) return;
 #pragma unroll
@@ -838,7 +902,11 @@ __global__ __launch_bounds__(NW * 64, (NW >= 8 ? 2 : 1)) void attn_dkdv_kernel(B
   lds_barrier();
   const bool wave_keys = kw0 < T;
 
-  for (int t = 0; t < ntiles; ++t) {
+  // masked diagonal tiles, unmasked interior, masked ragged tail tile; each loop
+  // is one straight-line body (both variants behind a branch spill).  Lanes with
+  // key >= T only pollute their own (never stored) dK/dV columns.
+  auto step = [&](int t, auto MASKED) {
+    constexpr bool MASK = decltype(MASKED)::value;
     // keep lane-derived addresses loop-variant: recomputed per tile instead of
     // hoisted into (spilled) registers across the whole loop
     asm volatile("" : "+v"(lane));
@@ -852,21 +920,42 @@ __global__ __launch_bounds__(NW * 64, (NW >= 8 ? 2 : 1)) void attn_dkdv_kernel(B
       const E* Dc = Db + buf * BQ * DV;
       const float* Lc = Lb + buf * NP;
       const float* Gc = Gb + buf * NP;
-      const bool needmask = (kw0 + 31 > q0) || (q0 + BQ > T) || (kw0 + 32 > T);
+      {
       f32x16 dpa = f32x16{};
       if constexpr (DK) {
+        if constexpr (sizeof(E) == 2) {
+          const int Ld = row_lane<DI::ROWB>(lane);
+          const char* dbase = reinterpret_cast<const char*>(Dc);
 #pragma unroll
-        for (int s = 0; s < NSV; ++s) dpa = O::mma(DI::row(Dc, c32, s, hf), vf[s], dpa);
+          for (int s = 0; s < NSV; ++s) dpa = O::mma(*reinterpret_cast<const frag*>(dbase + (Ld ^ (32 * s))), vf[s], dpa);
+        } else {
+#pragma unroll
+          for (int s = 0; s < NSV; ++s) dpa = O::mma(DI::row(Dc, c32, s, hf), vf[s], dpa);
+        }
       }
       f32x16 pc = f32x16{};
+      // rows q0 + rowof(r) > lim are masked: query < key, or past the end
+      const int lim_lo = krow - q0 - 4 * hf;          // masked if rowof_c < lim_lo (query < key)
+      const int lim_hi = T - 1 - q0 - 4 * hf;         // masked if rowof_c > lim_hi (query >= T)
 #pragma unroll
       for (int i = 0; i < N; ++i) {
         f32x16 sa = f32x16{};
         const E* Qi = Qc + i * BQ * HSP;
+        if constexpr (sizeof(E) == 2) {
+          const int Lq = row_lane<QI::ROWB>(lane), Lk = row_lane<KI::ROWB>(lane);
+          const char* qbase = reinterpret_cast<const char*>(Qi);
+          const char* kbase = reinterpret_cast<const char*>(Ks + i * BK * HS) + wave * 32 * KI::ROWB;
 #pragma unroll
-        for (int s = 0; s < NSQ; ++s)
-          sa = O::mma(QI::row(Qi, c32, s, hf), KI::row(Ks + i * BK * HS, wave * 32 + c32, s, hf), sa);
-        // sa[r] = S_i[q0 + rowof(r)][krow]; rows 4g..4g+3 of a lane are consecutive
+          for (int s = 0; s < NSQ; ++s)
+            sa = O::mma(*reinterpret_cast<const frag*>(qbase + (Lq ^ (32 * s))),
+                        *reinterpret_cast<const frag*>(kbase + (Lk ^ (32 * s))), sa);
+        } else {
+#pragma unroll
+          for (int s = 0; s < NSQ; ++s)
+            sa = O::mma(QI::row(Qi, c32, s, hf), KI::row(Ks + i * BK * HS, wave * 32 + c32, s, hf), sa);
+        }
+        // sa[r] = S_i[q0 + rowof(r)][krow]; rows 4g..4g+3 of a lane are consecutive.
+        // Gc holds c_i * delta_i (written by attn_dq): dS = P * (c_i dP - c_i delta_i)
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const f32x4 l4 = *reinterpret_cast<const f32x4*>(Lc + i * BQ + 8 * g + 4 * hf);
@@ -875,13 +964,14 @@ __global__ __launch_bounds__(NW * 64, (NW >= 8 ? 2 : 1)) void attn_dkdv_kernel(B
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const int r = 4 * g + j;
-            float pr = exp2_fast(fmaf(sa[r], p.sl2, -l4[j]));
-            if (needmask) {
-              const int q = q0 + rowof(r, hf);
-              if (krow > q || q >= T || krow >= T) pr = 0.f;
+            float arg = fmaf(sa[r], p.sl2, -l4[j]);
+            if constexpr (MASK) {
+              const int rc = (r & 3) + 8 * (r >> 2);
+              arg = (rc < lim_lo || rc > lim_hi) ? -INFINITY : arg;
             }
+            const float pr = exp2_fast(arg);
             if constexpr (DVV) pc[r] = fmaf(coef[i], pr, pc[r]);
-            if constexpr (DK) sa[r] = coef[i] * pr * (dpa[r] - d4[j]);
+            if constexpr (DK) sa[r] = pr * fmaf(coef[i], dpa[r], -d4[j]);
           }
         }
         if constexpr (DK) {
@@ -935,10 +1025,16 @@ __global__ __launch_bounds__(NW * 64, (NW >= 8 ? 2 : 1)) void attn_dkdv_kernel(B
             for (int s = 0; s < SPB; ++s) dv[d] = O::mma(DI::tr_perm(Dc, 0, s, hf, d * 32, lane), pc[s], dv[d]);
         }
       }
+      }
     }
     wait_vm(tile_pieces * max(0, min(NS - 2, ntiles - 2 - t)));
     lds_barrier();
-  }
+  };
+  const int thead = min(ntiles, (BK - 2) / BQ + 1);                  // q0 < kb0 + BK - 1
+  const int ttail = max(thead, ntiles - ((T - kb0) % BQ != 0 ? 1 : 0));  // q0 + BQ > T
+  for (int t = 0; t < thead; ++t) step(t, std::true_type{});
+  for (int t = thead; t < ttail; ++t) step(t, std::false_type{});
+  for (int t = ttail; t < ntiles; ++t) step(t, std::true_type{});
 
   if (!wave_keys || krow >= T) return;
   if constexpr (DK) {
