@@ -95,6 +95,24 @@ def cpu_baseline(T=4096, H=16, hs=64, reps=2):
                       f"{sec:.2f} s per sample; rate per algorithmic FLOP, same FLOP count as the GPU step"}
 
 
+def _pmc_traffic(kernel):
+    """HBM bytes per launch of ``kernel`` from the newest committed PMC summary
+    (profiles/*_pmc_traffic.json, written from separate rocprofv3 --pmc FETCH_SIZE /
+    WRITE_SIZE passes of this same command, FETCH_SIZE doubled per the gfx950
+    correction).  (None, None) when no summary exists."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))   # rNN_vM: newest last
+    for f in reversed(files):
+        try:
+            with open(f) as fh:
+                k = json.load(fh)["kernels"].get(kernel)
+        except (OSError, ValueError, KeyError):
+            continue
+        if k:
+            return k["traffic_bytes"], os.path.relpath(f, ROOT)
+    return None, None
+
+
 def kernel_bench(args, world, rank):
     from differential_transformer_replication_amd import ops
     from differential_transformer_replication_amd.diff_transformer import _layer_lambda_coef
@@ -140,6 +158,9 @@ def kernel_bench(args, world, rank):
         kernels[name] = {"ms": round(t, 4), "launches": n, "alg_tflops": round(flops[name] / t / 1e9, 2)}
     dom = max(kernels, key=lambda k: kernels[k]["ms"])
     achieved = kernels[dom]["alg_tflops"]
+    traffic, traffic_src = args.traffic, None
+    if traffic is None:
+        traffic, traffic_src = _pmc_traffic(dom)
     res = {
         "metric": METRIC, "value": round(value, 3), "unit": "TFLOP/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
@@ -152,7 +173,7 @@ def kernel_bench(args, world, rank):
         "kernels": kernels,
         "roofline": {"bound": "mfma", "kernel": dom, "achieved": achieved, "peak": PEAK_BF16_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
-                     "traffic": args.traffic},
+                     "traffic": traffic, "traffic_source": traffic_src},
     }
     return res
 
