@@ -796,8 +796,6 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_dq_kernel(BwdParams p) {
 }
 
 // --------------------------------------------------- backward: dK, dV ---
-template <class E> struct DkdvWaves { static constexpr int v = 8; };
-template <> struct DkdvWaves<float> { static constexpr int v = 4; };
 
 template <class E, int HS, int N, int DV, int NW>
 struct DkdvCfg {
@@ -810,6 +808,14 @@ struct DkdvCfg {
   static constexpr int nK = N * BK * HS;                   // the workgroup's K_i rows (B of S_i)
   static constexpr int NS = ring_stages(nK * (int)sizeof(E), (nQ + nD) * (int)sizeof(E) + 2 * NP * 4);
   static constexpr int bytes = (nK + NS * nQ + NS * nD) * (int)sizeof(E) + NS * 2 * NP * 4;
+};
+
+// widest key block (waves x 32 keys) whose K rows plus a 2+-stage query ring fit LDS
+template <class E, int HS, int N, int DV>
+struct DkdvWaves {
+  static constexpr int LIM = 160 * 1024;
+  static constexpr int v = (sizeof(E) == 2 && DkdvCfg<E, HS, N, DV, 8>::bytes <= LIM) ? 8
+                         : DkdvCfg<E, HS, N, DV, 4>::bytes <= LIM ? 4 : 2;
 };
 
 // accumulator budget -> whether dK and dV share one launch
@@ -1076,7 +1082,7 @@ struct Plan {
   static constexpr int DV = 2 * HS;
   using FP = FwdPick<E, HS, N>;
   using DP = DqPick<E, HS, N>;
-  static constexpr int KVW = DkdvWaves<E>::v;
+  static constexpr int KVW = DkdvWaves<E, HS, N, DV>::v;
   static constexpr bool ok = FP::ok && DP::ok && DkdvCfg<E, HS, N, DV, KVW>::bytes <= 160 * 1024;
 };
 
