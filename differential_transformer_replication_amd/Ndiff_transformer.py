@@ -195,7 +195,8 @@ class AlternatingDiffTransformer(nn.Module):
         logits = self.lm_head(self.ln_f(x))
         loss = None
         if targets is not None:
-            loss = F.cross_entropy(logits.view(B * T, -1), targets.view(B * T))
+            logits = logits.view(B * T, -1)             # reference returns (B*T, V) with targets
+            loss = F.cross_entropy(logits, targets.view(B * T))
         return logits, loss
 
     @torch.no_grad()

@@ -140,7 +140,7 @@ class ShardedWindows:
         idx = torch.randint(0, self.n, (self.world, self.mb), generator=self.gen)[self.rank].to(self.tokens.device)
         ar = torch.arange(self.T + 1, device=self.tokens.device)
         win = self.tokens[idx[:, None] + ar[None, :]]
-        return win[:, :-1], win[:, 1:]
+        return win[:, :-1].contiguous(), win[:, 1:].contiguous()   # TextDataset yields contiguous windows
 
 
 def load_tokens(cfg: TrainingConfig, device) -> torch.Tensor:

@@ -172,3 +172,18 @@ def test_lambda_side_effects_and_coefficients():
     for h, head in enumerate(na.heads):
         lam = head.get_lambda(2)
         assert torch.allclose(c[h], lam * torch.tensor([1.0, -1.0, 1.0]), rtol=1e-6)
+
+
+def test_control_model_cpu_matches_golden(golden):
+    """StandardTransformer end to end (logits returned as (B*T, V) with targets,
+    like the reference), loss and every parameter gradient."""
+    g = Golden(golden, "modelctrl")
+    m = C.StandardTransformer(97, 64, 4, 2, 24, 0.0).double()
+    m.load_state_dict(g.state_dict(torch.float64), strict=True)
+    idx = torch.from_numpy(g["idx"])
+    logits, loss = m(idx, torch.from_numpy(g["tgt"]))
+    assert tuple(logits.shape) == tuple(g["logits"].shape)
+    assert rel_err(logits, g["logits"]) < 1e-6
+    loss.backward()
+    for k, p in m.named_parameters():
+        assert rel_err(p.grad, g[f"grad::{k}"]) < 1e-5, k
