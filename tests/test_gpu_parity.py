@@ -56,6 +56,8 @@ CASES = [  # H, N, hs, T, rope
     (2, 2, 64, 129, False), (1, 2, 16, 7, False), (3, 2, 32, 200, False), (2, 3, 64, 65, True),
     (2, 4, 32, 97, True), (1, 1, 64, 64, True), (2, 2, 128, 130, False), (1, 4, 64, 70, False),
     (2, 2, 64, 1, False), (1, 2, 64, 256, True),
+    # long enough for the K/V ring to wrap many times under the staggered schedule
+    (1, 2, 64, 1100, False), (1, 1, 64, 777, False), (1, 3, 32, 1500, True),
 ]
 
 
@@ -95,6 +97,47 @@ def test_core_fwd_bwd(dtype, H, N, hs, T, rope):
     assert rel_err(gx[..., :nq], x64.grad[..., :nq]) < tol, "dQ"
     assert rel_err(gx[..., nq:2 * nq], x64.grad[..., nq:2 * nq]) < tol, "dK"
     assert rel_err(gx[..., 2 * nq:], x64.grad[..., 2 * nq:]) < tol, "dV"
+    assert rel_err(cg.grad.cpu(), c64.grad) < tol, "dcoef"
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_forced_rescale(dtype):
+    """The deferred online-softmax rescale (taken only when a row's running max
+    grows by more than 2^8 inside a block) is rare on random data, so force it
+    (cdna_hip_programming.md 5.4 rule 26): one key of branch 0 aligned with every
+    query makes that branch's max jump by ~10 (log2 units) at a late tile."""
+    ops = _ops()
+    H, N, hs, T, B = 2, 2, 64, 900, 1
+    g = torch.Generator().manual_seed(7)
+    W = ops.packed_width(H, N, hs, 2 * hs)
+    nq = H * N * hs
+    qkv = torch.randn(B, T, W, generator=g) * 0.3
+    u = torch.ones(hs) / math.sqrt(hs)
+    q = qkv[..., :nq].view(B, T, H, N, hs)
+    k = qkv[..., nq:2 * nq].view(B, T, H, N, hs)
+    q[:, :, :, 0] += 2.0 * u
+    # branch-0 score of key 700 ~ 60/sqrt(hs) = 7.5 for every query: a jump of ~10 (log2 units)
+    # over the running max, with P(key 700) ~ 0.7 -- not saturated, so dS = P(dP - delta) stays
+    # well conditioned under the bf16-stored O_i that delta is computed from
+    k[:, 700, :, 0] = 30.0 * u
+    k[:, 333, 1, 1] = -40.0 * u           # a large negative outlier in the other branch
+    coef = torch.tensor([[1.0, -0.4], [1.0, -0.6]])
+    do = torch.randn(B, T, H * 2 * hs, generator=g)
+    qkv_q = qkv.to(dtype).double()
+    x64 = qkv_q.clone().requires_grad_(True)
+    c64 = coef.double().clone().requires_grad_(True)
+    ref = _oracle_core(x64, c64, H, N, hs)
+    ref.backward(do.to(dtype).double())
+    xg = qkv.to(dtype).to(DEV).requires_grad_(True)
+    cg = coef.to(DEV).requires_grad_(True)
+    out = ops.diff_attention(xg, cg, H, N, hs)
+    out.backward(do.to(dtype).to(DEV))
+    torch.cuda.synchronize()
+    tol = TOL[dtype]
+    assert rel_err(out.float().cpu(), ref) < tol
+    gx = xg.grad.float().cpu()
+    for name, sl in (("dQ", slice(0, nq)), ("dK", slice(nq, 2 * nq)), ("dV", slice(2 * nq, None))):
+        assert rel_err(gx[..., sl], x64.grad[..., sl]) < tol, name
     assert rel_err(cg.grad.cpu(), c64.grad) < tol, "dcoef"
 
 
