@@ -113,11 +113,40 @@ def _pmc_traffic(kernel):
     return None, None
 
 
+def control_bench(B, H, hs, T, steps, warmup):
+    """control.py's standard causal attention (control.py:38-63) at equal F_fwd, on
+    PyTorch's own fused GPU attention (SDPA), bf16 fwd+bwd: the comparison line of
+    BASELINE configs[4].  Returns (ms per step, algorithmic TFLOP/s)."""
+    import torch.nn.functional as F
+    dev = torch.device("cuda", torch.cuda.current_device())
+    g = torch.Generator(device=dev).manual_seed(7)
+    q, k, v = (torch.randn(B, H, T, hs, device=dev, dtype=torch.bfloat16, generator=g).requires_grad_(True)
+               for _ in range(3))
+    do = torch.randn(B, H, T, hs, device=dev, dtype=torch.bfloat16, generator=g)
+
+    def step():
+        for t in (q, k, v):
+            t.grad = None
+        F.scaled_dot_product_attention(q, k, v, is_causal=True).backward(do)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    sec = (time.perf_counter() - t0) / steps
+    f = 3.0 * B * H * T * T * (hs + hs)          # N=1, dv=hs: F_fwd = B H T^2 (hs + dv)
+    return sec * 1e3, f / sec / 1e12
+
+
 def kernel_bench(args, world, rank):
     from differential_transformer_replication_amd import ops
     from differential_transformer_replication_amd.diff_transformer import _layer_lambda_coef
+    from differential_transformer_replication_amd.Ndiff_transformer import alternating_coefficients
     from differential_transformer_replication_amd._compat import lambda_init_value
-    B, H, hs, N, T = args.batch, 16, 64, 2, args.seq
+    B, H, hs, N, T = args.batch, args.heads, args.head_size, args.n_terms, args.seq
     dv = 2 * hs
     dev = torch.device("cuda", torch.cuda.current_device())
     W = ops.packed_width(H, N, hs, dv)
@@ -125,8 +154,12 @@ def kernel_bench(args, world, rank):
     qkv = torch.randn(B, T, W, device=dev, dtype=torch.bfloat16, generator=g).requires_grad_(True)
     do = torch.randn(B, T, H * dv, device=dev, dtype=torch.bfloat16, generator=g)
     g1 = torch.Generator(device=dev).manual_seed(1)
-    lam = [torch.randn(H, hs, device=dev, generator=g1) * 0.1 for _ in range(4)]
-    coef = _layer_lambda_coef(*lam, lambda_init_value(3, None))
+    if N == 2:
+        lam = [torch.randn(H, hs, device=dev, generator=g1) * 0.1 for _ in range(4)]
+        coef = _layer_lambda_coef(*lam, lambda_init_value(3, None))
+    else:                                        # N-term alternating coefficients (Ndiff_transformer.py:79-93)
+        lqs, lks = (torch.randn(H, N, hs, device=dev, generator=g1) * 0.1 for _ in range(2))
+        coef = alternating_coefficients(lqs, lks, float(lambda_init_value(3, None)))
 
     def step():
         qkv.grad = None
@@ -161,11 +194,14 @@ def kernel_bench(args, world, rank):
     traffic, traffic_src = args.traffic, None
     if traffic is None:
         traffic, traffic_src = _pmc_traffic(dom)
+    cfg2 = (B, H, hs, N, T) == (8, 16, 64, 2, 4096)
+    workload = ("cfg2: fused N=2 diff-attention core fwd+bwd (BASELINE configs[1])" if cfg2 else
+                f"diff-attention core fwd+bwd B={B} H={H} hs={hs} N={N} T={T}")
     res = {
         "metric": METRIC, "value": round(value, 3), "unit": "TFLOP/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
-        "config": {"workload": "cfg2: fused N=2 diff-attention core fwd+bwd (BASELINE configs[1])",
+        "config": {"workload": workload,
                    "batch_per_gpu": B, "global_batch": B * world, "heads": H, "head_size": hs, "dv": dv,
                    "seq_len": T, "n_terms": N, "causal": True,
                    "parallelism": f"batch-sharded replicas x{world} (no data-path collective)"},
@@ -175,6 +211,13 @@ def kernel_bench(args, world, rank):
                      "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
                      "traffic": traffic, "traffic_source": traffic_src},
     }
+    if args.control and rank == 0:
+        # control.py standard attention at equal F_fwd: 2*H heads of width hs, dv = hs (train.py:226)
+        cms, ctf = control_bench(B, 2 * H if N == 2 else H, hs, T, args.steps, args.warmup)
+        res["control"] = {"what": "control.py causal softmax attention, torch SDPA (ROCm fused attention), bf16 fwd+bwd, "
+                                  f"B={B} H={2 * H if N == 2 else H} hs=dv={hs} T={T}",
+                          "ms_per_step": round(cms, 4), "alg_tflops": round(ctf, 2),
+                          "diff_over_control_time": round(ms / cms, 3)}
     return res
 
 
@@ -186,6 +229,13 @@ def main():
     ap.add_argument("--mode", choices=["kernel", "train"], default="kernel")
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--seq", type=int, default=4096)
+    ap.add_argument("--heads", type=int, default=16)
+    ap.add_argument("--head-size", type=int, default=64)
+    ap.add_argument("--n-terms", type=int, default=2)
+    ap.add_argument("--control", action="store_true",
+                    help="kernel mode: also time control.py standard attention at equal F_fwd (BASELINE configs[4])")
+    ap.add_argument("--model", choices=["diff", "ndiff"], default="diff",
+                    help="train mode: cfg4 DiffTransformer (diff) or cfg3 AlternatingDiffTransformer (ndiff)")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--traffic", type=float, default=None,
                     help="HBM bytes per dominant-kernel launch from rocprofv3 PMC (profiles/)")
@@ -197,7 +247,9 @@ def main():
         from differential_transformer_replication_amd.train import train_bench
         res = train_bench(args, world, rank)
     if rank == 0:
-        if args.cpu_baseline == "auto" and world == 1:
+        default_kernel = args.mode == "kernel" and (args.batch, args.heads, args.head_size, args.n_terms,
+                                                     args.seq) == (8, 16, 64, 2, 4096)
+        if args.cpu_baseline == "auto" and world == 1 and default_kernel:
             res["cpu_baseline"] = cpu_baseline()
         else:
             res["cpu_baseline"] = None

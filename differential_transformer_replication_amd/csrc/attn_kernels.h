@@ -236,6 +236,16 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_s_barrier();
 }
 
+// Waves per SIMD a launch can keep resident given its LDS footprint (workgroups
+// per CU x waves per workgroup / 4 SIMDs), capped at the 2 the 256-register plans
+// target.  Where the LDS already limits a kernel to one wave per SIMD, its launch
+// bound says so and the wave gets the whole 512-entry register file (VGPRs +
+// AGPRs) instead of spilling at 256.
+constexpr int simd_waves(int nw, int bytes) {
+  const int w = (160 * 1024 / bytes) * nw / 4;
+  return w < 1 ? 1 : (w > 2 ? 2 : w);
+}
+
 // Ring depth for a per-tile footprint: as many stages (2..4) as the LDS leaves room for.
 constexpr int ring_stages(int fixed_bytes, int tile_bytes) {
   return (fixed_bytes + 4 * tile_bytes <= 160 * 1024) ? 4 : (fixed_bytes + 3 * tile_bytes <= 160 * 1024) ? 3 : 2;
@@ -261,6 +271,10 @@ struct FwdCfg {
   static constexpr int nV = BN * DVC;
   static constexpr int NS = ring_stages(nQ * (int)sizeof(E), (nK + nV) * (int)sizeof(E));
   static constexpr int bytes = (nQ + NS * nK + NS * nV) * (int)sizeof(E);
+  // rough VGPR count (accumulators, two key blocks of scores, P, Q fragments,
+  // addresses); a plan that fits 256 keeps the two-waves-per-SIMD bound
+  static constexpr int regs = N * DVC / 2 + N * 2 * 16 + N * 8 + (QREG ? N * HS / 4 : 0) + 48;
+  static constexpr int WPE = regs <= 256 ? 2 : simd_waves(NW, bytes);
 };
 
 template <class E, int HS, int N>
@@ -269,7 +283,9 @@ struct FwdPick {
   static constexpr int LIM = 160 * 1024;
   static constexpr int NWMAX = sizeof(E) == 2 ? 8 : 4;
   // widest workgroup with Q in LDS, else Q in registers
-  static constexpr bool q8 = NWMAX >= 8 && FwdCfg<E, HS, N, DVC, 8, false>::bytes <= LIM;
+  // an 8-wave plan past ~280 registers spills at two waves per SIMD: take 4 waves
+  static constexpr bool q8 = NWMAX >= 8 && FwdCfg<E, HS, N, DVC, 8, false>::bytes <= LIM &&
+                             FwdCfg<E, HS, N, DVC, 8, false>::regs <= 280;
   static constexpr bool q4 = FwdCfg<E, HS, N, DVC, 4, false>::bytes <= LIM;
   static constexpr int NW = q8 ? 8 : (q4 ? 4 : 4);
   static constexpr bool QREG = !(q8 || q4);
@@ -277,7 +293,7 @@ struct FwdPick {
 };
 
 template <class E, int HS, int N, int DVC, int NW, bool QREG>
-__global__ __launch_bounds__(NW * 64, 2) void attn_fwd_kernel(FwdParams p) {
+__global__ __launch_bounds__(NW * 64, (FwdCfg<E, HS, N, DVC, NW, QREG>::WPE)) void attn_fwd_kernel(FwdParams p) {
   using O = Ops<E>;
   using frag = typename O::frag;
   using QI = Img<E, HS>;
@@ -551,7 +567,8 @@ struct DqPick {
 };
 
 template <class E, int HS, int N, int DV, int NW, bool QREG, bool OUTF32>
-__global__ __launch_bounds__(NW * 64, 2) void attn_dq_kernel(BwdParams p) {
+__global__ __launch_bounds__(NW * 64, simd_waves(NW, DqCfg<E, HS, N, DV, NW, QREG>::bytes))
+void attn_dq_kernel(BwdParams p) {
   using O = Ops<E>;
   using frag = typename O::frag;
   using CF = DqCfg<E, HS, N, DV, NW, QREG>;
@@ -811,18 +828,24 @@ struct DkdvCfg {
 };
 
 // widest key block (waves x 32 keys) whose K rows plus a 2+-stage query ring fit LDS
-template <class E, int HS, int N, int DV>
-struct DkdvWaves {
-  static constexpr int LIM = 160 * 1024;
-  static constexpr int v = (sizeof(E) == 2 && DkdvCfg<E, HS, N, DV, 8>::bytes <= LIM) ? 8
-                         : DkdvCfg<E, HS, N, DV, 4>::bytes <= LIM ? 4 : 2;
-};
-
 // accumulator budget -> whether dK and dV share one launch
 template <int HS, int N, int DV>
 struct DkdvSplit {
   static constexpr int HSP = HS < 32 ? 32 : HS;
   static constexpr bool fused = (N * HSP / 2 + DV / 2) <= 160;
+};
+
+// widest key block (waves x 32 keys) whose K rows plus a 2+-stage query ring fit
+// LDS; 8 waves (two per SIMD, 256 registers each) only while the rough register
+// count of a launch (dK / dV accumulators, V fragments, scores) fits them
+template <class E, int HS, int N, int DV>
+struct DkdvWaves {
+  static constexpr int LIM = 160 * 1024;
+  static constexpr int HSP = HS < 32 ? 32 : HS;
+  static constexpr int regs8 = DkdvSplit<HS, N, DV>::fused ? N * HSP / 2 + DV / 2 + DV / 4 + 88
+                             : (N * HSP / 2 + DV / 4 > DV / 2 ? N * HSP / 2 + DV / 4 : DV / 2) + 88;
+  static constexpr int v = (sizeof(E) == 2 && DkdvCfg<E, HS, N, DV, 8>::bytes <= LIM && regs8 <= 256) ? 8
+                         : DkdvCfg<E, HS, N, DV, 4>::bytes <= LIM ? 4 : 2;
 };
 
 template <class E, int HS, int N, int DV, int NW, bool DK, bool DVV>

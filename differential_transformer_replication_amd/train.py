@@ -282,13 +282,21 @@ def train(cfg: TrainingConfig):
 # ----------------------------------------------------------------- bench ---
 CFG4 = dict(model="diff", vocab_size=12000, n_embd=1024, n_head=8, n_layer=20, block_size=2048, dropout=0.0,
             micro_batch_size=16)
+# BASELINE configs[2]: N-term model, ~125M at n_terms=4 (hs = 768 / (2*6) = 64)
+CFG3 = dict(model="ndiff", vocab_size=12000, n_embd=768, n_head=6, n_layer=10, block_size=2048, dropout=0.0,
+            micro_batch_size=16)
 
 
 def train_bench(args, world, rank):
     """bench.py --mode train: BASELINE configs[3] -- ~350M DiffTransformer
     (12000, 1024, 8, 20, 2048), micro-batch 16 x 2048 per GPU, bf16 autocast,
-    AdamW, DP all-reduce.  value = tokens/s over all ranks."""
-    cfg = TrainingConfig(**CFG4, warmup_iters=100, max_iters=10_000, dtype="bf16")
+    AdamW, DP all-reduce.  value = tokens/s over all ranks.  With --model ndiff:
+    BASELINE configs[2] -- AlternatingDiffTransformer(12000, 768, 6, 10, 2048,
+    n_terms=--n-terms), micro-batch 16 x 2048."""
+    arch = getattr(args, "model", "diff")
+    base = CFG3 if arch == "ndiff" else CFG4
+    extra = {"n_terms": args.n_terms} if arch == "ndiff" else {}
+    cfg = TrainingConfig(**base, **extra, warmup_iters=100, max_iters=10_000, dtype="bf16")
     dev = torch.device("cuda", torch.cuda.current_device())
     torch.manual_seed(cfg.seed)
     model = build_model(cfg).to(dev)
@@ -318,7 +326,9 @@ def train_bench(args, world, rank):
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
             "data": "synthetic", "final_loss": float(loss),
-            "config": {"workload": "cfg4: DiffTransformer(12000,1024,8,20,2048) DP training step",
+            "config": {"workload": (f"cfg3: AlternatingDiffTransformer(12000,768,6,10,2048,n_terms={cfg.n_terms}) "
+                                    "training step" if arch == "ndiff" else
+                                    "cfg4: DiffTransformer(12000,1024,8,20,2048) DP training step"),
                        "params": nparams, "micro_batch_per_gpu": cfg.micro_batch_size,
                        "global_batch": cfg.micro_batch_size * world, "seq_len": cfg.block_size,
                        "parallelism": f"dp{world} (bucketed RCCL all-reduce, {cfg.bucket_cap_mb} MB buckets)"}}
