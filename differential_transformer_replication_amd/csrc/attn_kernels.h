@@ -406,15 +406,36 @@ __global__ __launch_bounds__(NW * 64, (FwdCfg<E, HS, N, DVC, NW, QREG>::WPE)) vo
             const char* qbase = reinterpret_cast<const char*>(Qs + i * BM * HS) + wave * 32 * QI::ROWB;
 #pragma unroll
             for (int kb = 0; kb < NKB; ++kb) sa[kb] = f32x16{};
+            if constexpr (NSQ * (NKB + 1) <= 12) {
+              // every operand read of this branch's S^T issued ahead of its MFMA chain,
+              // so the chain waits on the LDS latency once instead of per k-step
+              // (head sizes <= 64; at 128 the 24 fragments do not fit the registers)
+              frag kfr[NKB][NSQ], qfr[NSQ];
 #pragma unroll
-            for (int s = 0; s < NSQ; ++s) {
-              const int o = Lr ^ (32 * s);
-              frag qb;
-              if constexpr (QREG) qb = qf[i][s];
-              else qb = *reinterpret_cast<const frag*>(qbase + o);
+              for (int s = 0; s < NSQ; ++s) {
+                const int o = Lr ^ (32 * s);
+                if constexpr (QREG) qfr[s] = qf[i][s];
+                else qfr[s] = *reinterpret_cast<const frag*>(qbase + o);
 #pragma unroll
-              for (int kb = 0; kb < NKB; ++kb)
-                sa[kb] = O::mma(*reinterpret_cast<const frag*>(kbase + kb * 32 * KI::ROWB + o), qb, sa[kb]);
+                for (int kb = 0; kb < NKB; ++kb) kfr[kb][s] = *reinterpret_cast<const frag*>(kbase + kb * 32 * KI::ROWB + o);
+              }
+#pragma unroll
+              for (int s = 0; s < NSQ; ++s)
+#pragma unroll
+                for (int kb = 0; kb < NKB; ++kb) sa[kb] = O::mma(kfr[kb][s], qfr[s], sa[kb]);
+              __builtin_amdgcn_sched_group_barrier(0x100, NSQ * (NKB + (QREG ? 0 : 1)), 0);
+              __builtin_amdgcn_sched_group_barrier(0x008, NSQ * NKB, 0);
+            } else {
+#pragma unroll
+              for (int s = 0; s < NSQ; ++s) {
+                const int o = Lr ^ (32 * s);
+                frag qb;
+                if constexpr (QREG) qb = qf[i][s];
+                else qb = *reinterpret_cast<const frag*>(qbase + o);
+#pragma unroll
+                for (int kb = 0; kb < NKB; ++kb)
+                  sa[kb] = O::mma(*reinterpret_cast<const frag*>(kbase + kb * 32 * KI::ROWB + o), qb, sa[kb]);
+              }
             }
           } else {
 #pragma unroll
@@ -974,10 +995,17 @@ __global__ __launch_bounds__(NW * 64, (NW >= 8 ? 2 : 1)) void attn_dkdv_kernel(B
           const int Lq = row_lane<QI::ROWB>(lane), Lk = row_lane<KI::ROWB>(lane);
           const char* qbase = reinterpret_cast<const char*>(Qi);
           const char* kbase = reinterpret_cast<const char*>(Ks + i * BK * HS) + wave * 32 * KI::ROWB;
+          // operand reads of this branch's S ahead of its MFMA chain (see attn_fwd_kernel)
+          frag qfr[NSQ], kfr[NSQ];
 #pragma unroll
-          for (int s = 0; s < NSQ; ++s)
-            sa = O::mma(*reinterpret_cast<const frag*>(qbase + (Lq ^ (32 * s))),
-                        *reinterpret_cast<const frag*>(kbase + (Lk ^ (32 * s))), sa);
+          for (int s = 0; s < NSQ; ++s) {
+            qfr[s] = *reinterpret_cast<const frag*>(qbase + (Lq ^ (32 * s)));
+            kfr[s] = *reinterpret_cast<const frag*>(kbase + (Lk ^ (32 * s)));
+          }
+#pragma unroll
+          for (int s = 0; s < NSQ; ++s) sa = O::mma(qfr[s], kfr[s], sa);
+          __builtin_amdgcn_sched_group_barrier(0x100, 2 * NSQ, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, NSQ, 0);
         } else {
 #pragma unroll
           for (int s = 0; s < NSQ; ++s)
