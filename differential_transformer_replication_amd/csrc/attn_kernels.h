@@ -543,7 +543,7 @@ __global__ __launch_bounds__(NW * 64, (FwdCfg<E, HS, N, DVC, NW, QREG>::WPE)) vo
     const float lt = wave_sum_halves(l[i]);
     inv[i] = 1.f / lt;
     if (dc0 == 0 && hf == 0)
-      p.lse[(((int64_t)i * p.B + b) * p.H + hh) * T + qrow] = m[i] + __builtin_log2f(lt);
+      p.lse[(((int64_t)i * p.B + b) * p.H + hh) * T + qrow] = -(m[i] + __builtin_log2f(lt));   // stored negated
   }
   E* go = reinterpret_cast<E*>(p.o.p) + b * p.o.sb + (int64_t)qrow * p.o.st + hh * p.o.sh + dc0;
   E* gob = reinterpret_cast<E*>(p.obr.p) + b * p.obr.sb + (int64_t)qrow * p.obr.st + hh * p.obr.sh + dc0;
@@ -774,7 +774,7 @@ void attn_dq_kernel(BwdParams p) {
           for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-              float arg = fmaf(sa[kb][r], p.sl2, -li);
+              float arg = fmaf(sa[kb][r], p.sl2, li);      // li = -LSE
               if constexpr (MASK) arg = (kb * 32 + (r & 3) + 8 * (r >> 2) > lim) ? -INFINITY : arg;
               sa[kb][r] = exp2_fast(arg) * fmaf(ci, dp[kb][r], -cdi);
             }
@@ -833,6 +833,94 @@ void attn_dq_kernel(BwdParams p) {
       }
 }
 
+// one LDS-DMA piece: SZ bytes per lane from byte voff of the buffer [base, base + bytes)
+// (zeros past its end) to lds + SZ * lane.  base, bytes and lds are wave-uniform.
+// (The transfer size is a literal in each helper: the host pass of hipcc rejects
+// a template-dependent size here.)
+__device__ __forceinline__ void buf_lds16(const void* base, uint32_t bytes, char* lds, uint32_t voff) {
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)lds, 16, voff, 0, 0, 0);
+}
+__device__ __forceinline__ void buf_lds4(const void* base, uint32_t bytes, char* lds, uint32_t voff) {
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)lds, 4, voff, 0, 0, 0);
+}
+
+// One query tile of the key-major backward -- Q_i rows, dO rows, LSE rows and
+// (with DELTA) c*delta rows -- streamed into one ring stage by buffer_load ... lds.
+// Stage layout: [N][BQ][HS] Q image | [BQ][DV] dO image | [NP] lse | [NP] c*delta.
+// Every per-lane source offset is computed once (init); a tile then costs only
+// scalar descriptor setup.  Rows past T read as zeros (and are masked).
+template <class E, int HS, int N, int DV, int NW, bool DELTA, int BQ_ = 32>
+struct TileRing {
+  static constexpr int ES = (int)sizeof(E), BQ = BQ_;
+  static constexpr int NP = (N * BQ + 63) / 64 * 64;
+  static constexpr int QB = BQ * HS * ES, DB = BQ * DV * ES;
+  static constexpr int OFF_D = N * QB, OFF_L = OFF_D + DB, OFF_G = OFF_L + NP * 4, SB = OFF_G + NP * 4;
+  static constexpr int PQ = N * QB / 1024, PD = DB / 1024, PL = NP / 64;
+  static constexpr int NPC = PQ + PD + (DELTA ? 2 : 1) * PL;     // DMA pieces per stage
+  static constexpr int MYP = (NPC + NW - 1) / NW;                  // piece j goes to wave j % NW
+  static constexpr bool ok = ES == 2 && HS >= 32 && QB % 1024 == 0 && DB % 1024 == 0;
+
+  __device__ static int pieces(int wave) { return NPC / NW + (wave < NPC % NW ? 1 : 0); }
+
+  // byte offset of lane's 16 (or 4) bytes of piece j from the tile's row base
+  __device__ static uint32_t offq(const BwdParams& p, int j, int lane) {           // j < PQ
+    using QI = Img<E, HS>;
+    const int i = j / (QB / 1024), pb = (j % (QB / 1024)) * 1024 + lane * 16;
+    const int r = pb / QI::ROWB, c = ((pb % QI::ROWB) >> 4) ^ swz<QI::ROWB>(r);
+    return (uint32_t)(r * (uint32_t)(p.q.st * ES) + (uint32_t)(i * p.q.si * ES) + c * 16);
+  }
+  __device__ static uint32_t offd(const BwdParams& p, int j, int lane) {           // PQ <= j < PQ + PD
+    using DI = Img<E, DV>;
+    const int pb = (j - PQ) * 1024 + lane * 16;
+    const int r = pb / DI::ROWB, c = ((pb % DI::ROWB) >> 4) ^ swz<DI::ROWB>(r);
+    return (uint32_t)(r * (uint32_t)(p.dout.st * ES) + c * 16);
+  }
+  __device__ static uint32_t offr(int j, int lane, int64_t bstride) {              // row-vector pieces
+    const int e = ((j - PQ - PD) % PL) * 64 + lane;
+    const int i = min(e / BQ, N - 1), r = e % BQ;
+    return (uint32_t)((i * (uint32_t)bstride + r) * 4);
+  }
+  // gq / gdo: (b, h) bases; lse / delta: (b, h) row-vector bases of branch 0.
+  // Wave w issues pieces j = u * NW + w; a slot u whose NW pieces are all of one
+  // kind is resolved at compile time (no per-piece scalar branching).
+  __device__ static void issue(const BwdParams& p, const E* gq, const E* gdo, const float* lse, const float* delta,
+                               int64_t bstride, int q0, int T, char* st0, int wave, int lane) {
+    const int rows = T - q0;                       // > 0 for every issued tile
+    const E* bq = gq + (int64_t)q0 * p.q.st;
+    const E* bd = gdo + (int64_t)q0 * p.dout.st;
+    const uint32_t nq = (uint32_t)rows * (uint32_t)(p.q.st * ES), nd = (uint32_t)rows * (uint32_t)(p.dout.st * ES);
+    const uint32_t nl = (uint32_t)(((N - 1) * bstride + rows) * 4);
+    sfor<MYP>([&](auto U) {
+      constexpr int u = decltype(U)::value;
+      const int j = u * NW + wave;
+      if constexpr ((u + 1) * NW <= PQ) {
+        buf_lds16(bq, nq, st0 + j * 1024, offq(p, j, lane));
+      } else if constexpr (u * NW >= PQ && (u + 1) * NW <= PQ + PD) {
+        buf_lds16(bd, nd, st0 + OFF_D + (j - PQ) * 1024, offd(p, j, lane));
+      } else {
+        if (j < PQ) buf_lds16(bq, nq, st0 + j * 1024, offq(p, j, lane));
+        else if (j < PQ + PD) buf_lds16(bd, nd, st0 + OFF_D + (j - PQ) * 1024, offd(p, j, lane));
+        else if (j < PQ + PD + PL) buf_lds4(lse + q0, nl, st0 + OFF_L + (j - PQ - PD) * 256, offr(j, lane, bstride));
+        else if (j < NPC) buf_lds4(delta + q0, nl, st0 + OFF_G + (j - PQ - PD - PL) * 256, offr(j, lane, bstride));
+      }
+    });
+  }
+};
+
+// The buffer descriptors cover [row base, T rows) of each operand: every branch's
+// columns must lie inside one row stride and the extents must fit the 32-bit
+// record count.  Otherwise the DMA-by-address staging runs.
+inline bool ring_layout_ok(const BwdParams& p, int es) {
+  const int64_t qs = p.q.st, ds = p.dout.st;
+  if (qs <= 0 || ds <= 0 || p.q.si < 0) return false;
+  if ((int64_t)(p.N - 1) * p.q.si + p.HS > qs || p.DV > ds) return false;
+  if ((int64_t)p.T * qs * es >= (1ll << 31) || (int64_t)p.T * ds * es >= (1ll << 31)) return false;
+  if ((int64_t)p.N * p.B * p.H * p.T * 4 >= (1ll << 31)) return false;
+  return true;
+}
+
 // --------------------------------------------------- backward: dK, dV ---
 
 template <class E, int HS, int N, int DV, int NW>
@@ -869,7 +957,7 @@ struct DkdvWaves {
                          : DkdvCfg<E, HS, N, DV, 4>::bytes <= LIM ? 4 : 2;
 };
 
-template <class E, int HS, int N, int DV, int NW, bool DK, bool DVV>
+template <class E, int HS, int N, int DV, int NW, bool DK, bool DVV, bool SRD>
 __global__ __launch_bounds__(NW * 64, (NW >= 8 ? 2 : 1)) void attn_dkdv_kernel(BwdParams p) {
   using O = Ops<E>;
   using frag = typename O::frag;
@@ -889,6 +977,10 @@ __global__ __launch_bounds__(NW * 64, (NW >= 8 ? 2 : 1)) void attn_dkdv_kernel(B
   E* Db = Qb + NS * CF::nQ;               // [NS][BQ][DV]
   float* Lb = reinterpret_cast<float*>(Db + NS * CF::nD);  // [NS][NP] lse
   float* Gb = Lb + NS * NP;                                 // [NS][NP] delta
+  // SRD: the ring is instead NS stages of TileRing's layout, filled by buffer_load ... lds
+  using RG = TileRing<E, HS, N, DV, NW, DK>;
+  char* ringb = reinterpret_cast<char*>(Qb);
+  static_assert(!SRD || (RG::ok && RG::SB * NS <= CF::bytes - CF::nK * (int)sizeof(E)), "ring layout");
 
   // wave index is wave-uniform: make it provably so (SGPR), or every branch on it
   // becomes an exec-masked divergent branch
@@ -924,12 +1016,16 @@ __global__ __launch_bounds__(NW * 64, (NW >= 8 ? 2 : 1)) void attn_dkdv_kernel(B
   }
 
   auto stage_q = [&](int q0, int buf) {
+    if constexpr (SRD) {
+      RG::issue(p, gq, gdo, p.lse + rowvec, p.delta + rowvec, bstride, q0, T, ringb + buf * RG::SB, wave, lane);
+    } else {
 #pragma unroll
-    for (int i = 0; i < N; ++i)
-      stage<E, HSP, BQ, HS, NTHR>(Qb + (buf * N + i) * BQ * HSP, gq + i * p.q.si, p.q.st, q0, T - 1, tid);
-    stage<E, DV, BQ, DV, NTHR>(Db + buf * BQ * DV, gdo, p.dout.st, q0, T - 1, tid);
-    stage_rows<N, BQ, NTHR>(Lb + buf * NP, p.lse + rowvec, bstride, q0, T - 1, tid);
-    if constexpr (DK) stage_rows<N, BQ, NTHR>(Gb + buf * NP, p.delta + rowvec, bstride, q0, T - 1, tid);
+      for (int i = 0; i < N; ++i)
+        stage<E, HSP, BQ, HS, NTHR>(Qb + (buf * N + i) * BQ * HSP, gq + i * p.q.si, p.q.st, q0, T - 1, tid);
+      stage<E, DV, BQ, DV, NTHR>(Db + buf * BQ * DV, gdo, p.dout.st, q0, T - 1, tid);
+      stage_rows<N, BQ, NTHR>(Lb + buf * NP, p.lse + rowvec, bstride, q0, T - 1, tid);
+      if constexpr (DK) stage_rows<N, BQ, NTHR>(Gb + buf * NP, p.delta + rowvec, bstride, q0, T - 1, tid);
+    }
   };
 
   f32x16 dk[DK ? N : 1][NHB];
@@ -944,8 +1040,9 @@ __global__ __launch_bounds__(NW * 64, (NW >= 8 ? 2 : 1)) void attn_dkdv_kernel(B
   const int ntiles = kb0 < T ? (T - kb0 + BQ - 1) / BQ : 0;
 #pragma unroll
   for (int i = 0; i < N; ++i) stage<E, HS, BK, HS, NTHR>(Ks + i * BK * HS, gk + i * p.k.si, p.k.st, kb0, T - 1, tid);
-  const int tile_pieces = N * stage_pieces<E, HSP, BQ, HS, NW>(wave) + stage_pieces<E, DV, BQ, DV, NW>(wave) +
-                          rows_pieces<N, BQ, NW>(wave) * (DK ? 2 : 1);
+  const int tile_pieces = SRD ? RG::pieces(wave)
+                              : N * stage_pieces<E, HSP, BQ, HS, NW>(wave) + stage_pieces<E, DV, BQ, DV, NW>(wave) +
+                                    rows_pieces<N, BQ, NW>(wave) * (DK ? 2 : 1);
   for (int j = 0; j < NS - 1; ++j)
     if (j < ntiles) stage_q(kb0 + j * BQ, j);
   wait_vm(tile_pieces * max(0, min(NS - 1, ntiles) - 1));
@@ -966,10 +1063,11 @@ __global__ __launch_bounds__(NW * 64, (NW >= 8 ? 2 : 1)) void attn_dkdv_kernel(B
     const int q0 = kb0 + t * BQ;
     if (t + NS - 1 < ntiles) stage_q(q0 + (NS - 1) * BQ, (t + NS - 1) % NS);
     if (wave_keys && q0 + BQ - 1 >= kw0) {
-      const E* Qc = Qb + buf * N * BQ * HSP;
-      const E* Dc = Db + buf * BQ * DV;
-      const float* Lc = Lb + buf * NP;
-      const float* Gc = Gb + buf * NP;
+      const char* sg = ringb + buf * RG::SB;
+      const E* Qc = SRD ? reinterpret_cast<const E*>(sg) : Qb + buf * N * BQ * HSP;
+      const E* Dc = SRD ? reinterpret_cast<const E*>(sg + RG::OFF_D) : Db + buf * BQ * DV;
+      const float* Lc = SRD ? reinterpret_cast<const float*>(sg + RG::OFF_L) : Lb + buf * NP;
+      const float* Gc = SRD ? reinterpret_cast<const float*>(sg + RG::OFF_G) : Gb + buf * NP;
       {
       f32x16 dpa = f32x16{};
       if constexpr (DK) {
@@ -1021,7 +1119,7 @@ __global__ __launch_bounds__(NW * 64, (NW >= 8 ? 2 : 1)) void attn_dkdv_kernel(B
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const int r = 4 * g + j;
-            float arg = fmaf(sa[r], p.sl2, -l4[j]);
+            float arg = fmaf(sa[r], p.sl2, l4[j]);      // l4 = -LSE
             if constexpr (MASK) {
               const int rc = (r & 3) + 8 * (r >> 2);
               arg = (rc < lim_lo || rc > lim_hi) ? -INFINITY : arg;
@@ -1120,6 +1218,278 @@ __global__ __launch_bounds__(NW * 64, (NW >= 8 ? 2 : 1)) void attn_dkdv_kernel(B
   }
 }
 
+// ------------------------------------ backward: dK, dV, one wave per SIMD ---
+//
+// Same math and operand maps as attn_dkdv_kernel, re-planned for the 512-entry
+// register file of a single wave per SIMD (4-wave workgroup, 128 keys):
+//  * K_i and V key rows live in registers for the whole loop (B operands of S_i
+//    and dP), so the only LDS reads per query tile are the streamed Q_i / dO /
+//    LSE / c*delta and their transposed reads;
+//  * every per-lane LDS and global offset is computed once, before the loop;
+//  * tiles arrive by buffer_load ... lds through per-tile buffer descriptors built
+//    in SGPRs (row base and byte extent), so a tile costs no vector address math
+//    and rows past T read as zeros (then masked) instead of being clamped.
+template <class E, int HS, int N, int DV>
+struct Dkdv4Cfg {
+  static constexpr int NW = 4, BQ = 64, BK = NW * 32, NS = 3;
+  using R = TileRing<E, HS, N, DV, NW, true, BQ>;
+  static constexpr int bytes = NS * R::SB;
+  // rough register count: dK/dV accumulators, K/V fragments, two 32-row sub-tiles of scores / operands
+  static constexpr int regs = N * HS / 2 + DV / 2 + DV / 4 + N * HS / 4 +      // dk, dv, vf, kf
+                              2 * (N * 16 + 16 + N * 16) +                       // sa, dpa, delta rows
+                              N * HS / 4 + DV / 4 + 2 * (N + 1) * 8 + 48;        // operand rows, packs, misc
+  static constexpr bool ok = R::ok && HS <= 64 && bytes <= 160 * 1024 && regs <= 520;
+};
+
+// One wave per SIMD: 4 waves x 32 keys; each step consumes a 64-row query tile as
+// two 32-row sub-tiles whose MFMA chains and softmax VALU are independent, so the
+// scheduler can run one sub-tile's VALU beside the other's MFMAs.
+//  * K_i (pre-multiplied by scale*log2e, once) and V rows stay in registers;
+//  * the S accumulators start at the stored -LSE rows, so P = exp2(S') directly;
+//  * tiles arrive through TileRing (descriptor-based LDS-DMA, no per-tile vector math).
+template <class E, int HS, int N, int DV>
+__global__ __launch_bounds__(256, 1) void attn_dkdv4_kernel(BwdParams p) {
+  using O = Ops<E>;
+  using frag = typename O::frag;
+  using CF = Dkdv4Cfg<E, HS, N, DV>;
+  using R = typename CF::R;
+  constexpr int BQ = CF::BQ, BK = CF::BK, NS = CF::NS, SB = R::SB;
+  constexpr int QB = R::QB, OFF_D = R::OFF_D, OFF_L = R::OFF_L, OFF_G = R::OFF_G;
+  using QI = Img<E, HS>;
+  using DI = Img<E, DV>;
+  constexpr int KS = O::KSTEP;
+  constexpr int NSQ = HS / KS, NSV = DV / KS, NHB = HS / 32, NVB = DV / 32;
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63, hf = lane >> 5, c32 = lane & 31;
+  const int nblk = gridDim.x * gridDim.y * gridDim.z;
+  const int lin = xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z), nblk);
+  const int kblk = lin % gridDim.x, hh = (lin / gridDim.x) % gridDim.y, b = lin / (gridDim.x * gridDim.y);
+  const int T = p.T;
+  const int kb0 = kblk * BK, kw0 = kb0 + wave * 32;
+  const int krow = kw0 + c32;
+
+  const E* gq = reinterpret_cast<const E*>(p.q.p) + b * p.q.sb + hh * p.q.sh;
+  const E* gk = reinterpret_cast<const E*>(p.k.p) + b * p.k.sb + hh * p.k.sh;
+  const E* gv = reinterpret_cast<const E*>(p.v.p) + b * p.v.sb + hh * p.v.sh;
+  const E* gdo = reinterpret_cast<const E*>(p.dout.p) + b * p.dout.sb + hh * p.dout.sh;
+  const int64_t rowvec = ((int64_t)b * p.H + hh) * T;
+  const int64_t bstride = (int64_t)p.B * p.H * T;
+
+  float coef[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) coef[i] = p.coef[hh * N + i];
+
+  // this wave's key rows: sl2 * K_i (B of S'_i = Q_i (sl2 K_i)^T) and V (B of dP = dO V^T)
+  frag kf[N][NSQ], vf[NSV];
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+#pragma unroll
+    for (int s = 0; s < NSQ; ++s) {
+      frag k = krow < T ? O::load_global(gk + (int64_t)krow * p.k.st + i * p.k.si + s * KS + hf * O::KH) : O::zero();
+#pragma unroll
+      for (int j = 0; j < 8; ++j) k[j] = (E)((float)k[j] * p.sl2);
+      kf[i][s] = k;
+    }
+#pragma unroll
+  for (int s = 0; s < NSV; ++s)
+    vf[s] = krow < T ? O::load_global(gv + (int64_t)krow * p.v.st + s * KS + hf * O::KH) : O::zero();
+
+  const int mypieces = R::pieces(wave);
+  const int ntiles = kb0 < T ? (T - kb0 + BQ - 1) / BQ : 0;
+  auto stage = [&](int t, int buf) {
+    R::issue(p, gq, gdo, p.lse + rowvec, p.delta + rowvec, bstride, kb0 + t * BQ, T, smem + buf * SB, wave, lane);
+  };
+
+  // loop-invariant LDS read offsets (bytes within a stage, sub-tile 0)
+  uint32_t lq[NSQ], ld[NSV], tq[NHB][2], td[NVB][2];
+  {
+    const int Lq = row_lane<QI::ROWB>(lane), Ld = row_lane<DI::ROWB>(lane);
+    const int Tq = tr_lane<QI::ROWB>(lane), Td = tr_lane<DI::ROWB>(lane);
+#pragma unroll
+    for (int s = 0; s < NSQ; ++s) lq[s] = Lq ^ (32 * s);
+#pragma unroll
+    for (int s = 0; s < NSV; ++s) ld[s] = OFF_D + (Ld ^ (32 * s));
+#pragma unroll
+    for (int d = 0; d < NHB; ++d) { tq[d][0] = Tq ^ (64 * d); tq[d][1] = Tq ^ (64 * d + 32); }
+#pragma unroll
+    for (int d = 0; d < NVB; ++d) { td[d][0] = OFF_D + (Td ^ (64 * d)); td[d][1] = OFF_D + (Td ^ (64 * d + 32)); }
+  }
+  const int lrow = 16 * hf;          // + 32 g bytes: rows 8g + 4hf of a 32-row vector
+
+  f32x16 dk[N][NHB], dv[NVB];
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+#pragma unroll
+    for (int d = 0; d < NHB; ++d) dk[i][d] = f32x16{};
+#pragma unroll
+  for (int d = 0; d < NVB; ++d) dv[d] = f32x16{};
+  // dK / dV accumulators belong in AGPRs (only MFMAs touch them); the per-tile
+  // score accumulators in VGPRs, where the softmax VALU reads them
+  auto pin_acc = [&]() {
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+#pragma unroll
+      for (int d = 0; d < NHB; ++d) asm volatile("" : "+a"(dk[i][d]));
+#pragma unroll
+    for (int d = 0; d < NVB; ++d) asm volatile("" : "+a"(dv[d]));
+    // K / V fragments are MFMA B operands only: AGPRs too
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+#pragma unroll
+      for (int s = 0; s < NSQ; ++s) asm volatile("" : "+a"(kf[i][s]));
+#pragma unroll
+    for (int s = 0; s < NSV; ++s) asm volatile("" : "+a"(vf[s]));
+  };
+  pin_acc();
+
+  for (int j = 0; j < NS - 1; ++j)
+    if (j < ntiles) stage(j, j);
+  wait_vm(mypieces * max(0, min(NS - 1, ntiles) - 1));
+  lds_barrier();
+  const bool wave_keys = kw0 < T;
+  const unsigned sbase = lds_addr(smem);
+
+  auto step = [&](int t, auto MASKED) {
+    constexpr bool MASK = decltype(MASKED)::value;
+    const int buf = t % NS;
+    const int q0 = kb0 + t * BQ;
+    if (t + NS - 1 < ntiles) stage(t + NS - 1, (t + NS - 1) % NS);
+    if (wave_keys && q0 + BQ - 1 >= kw0) {
+      const char* st0 = smem + buf * SB;
+      const unsigned sa0 = sbase + buf * SB;
+      // ---- MFMA chains of both sub-tiles: S'_i = -LSE_i + Q_i (sl2 K_i)^T, dP = dO V^T
+      f32x16 sa[2][N], dpa[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        frag qr[N][NSQ], dr[NSV];
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+#pragma unroll
+          for (int s = 0; s < NSQ; ++s) qr[i][s] = *reinterpret_cast<const frag*>(st0 + i * QB + u * 32 * QI::ROWB + lq[s]);
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const f32x4 l4 = *reinterpret_cast<const f32x4*>(st0 + OFF_L + (i * BQ + 32 * u) * 4 + 32 * g + lrow);
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) sa[u][i][4 * g + jj] = l4[jj];
+          }
+        }
+#pragma unroll
+        for (int s = 0; s < NSV; ++s) dr[s] = *reinterpret_cast<const frag*>(st0 + u * 32 * DI::ROWB + ld[s]);
+#pragma unroll
+        for (int i = 0; i < N; ++i)
+#pragma unroll
+          for (int s = 0; s < NSQ; ++s) sa[u][i] = O::mma(qr[i][s], kf[i][s], sa[u][i]);
+        dpa[u] = f32x16{};
+#pragma unroll
+        for (int s = 0; s < NSV; ++s) dpa[u] = O::mma(dr[s], vf[s], dpa[u]);
+#pragma unroll
+        for (int i = 0; i < N; ++i) asm volatile("" : "+v"(sa[u][i]));
+        asm volatile("" : "+v"(dpa[u]));
+      }
+      // ---- softmax side per sub-tile: P_i = exp2(S'_i); pc = sum_i c_i P_i; dS_i = P_i (c_i dP - c_i delta_i)
+      frag pk[2][2], ds[2][N][2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int lim_lo = krow - q0 - 32 * u - 4 * hf;     // masked if row < lim_lo (query < key)
+        const int lim_hi = T - 1 - q0 - 32 * u - 4 * hf;    // masked if row > lim_hi (query >= T)
+        f32x16 pc;
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const f32x4 d4 = *reinterpret_cast<const f32x4*>(st0 + OFF_G + (i * BQ + 32 * u) * 4 + 32 * g + lrow);
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+              const int r = 4 * g + jj;
+              float pr = exp2_fast(sa[u][i][r]);
+              if constexpr (MASK) {
+                const int rc = (r & 3) + 8 * (r >> 2);
+                pr = (rc < lim_lo || rc > lim_hi) ? 0.f : pr;
+              }
+              pc[r] = i == 0 ? coef[0] * pr : fmaf(coef[i], pr, pc[r]);
+              sa[u][i][r] = pr * fmaf(coef[i], dpa[u][r], -d4[jj]);
+            }
+          }
+          ds[u][i][0] = O::template pack<0>(sa[u][i]);
+          ds[u][i][1] = O::template pack<1>(sa[u][i]);
+        }
+        pk[u][0] = O::template pack<0>(pc);
+        pk[u][1] = O::template pack<1>(pc);
+      }
+      // ---- dV^T += dO^T pc (transposed dO reads, k = the 64 query rows)
+#pragma unroll
+      for (int d = 0; d < NVB; ++d) {
+        lds64 r[2][4];
+        tr_issue<DI::ROWB, 0>(r[0], sa0 + td[d][0], sa0 + td[d][1]);
+        tr_issue<DI::ROWB, 32>(r[1], sa0 + td[d][0], sa0 + td[d][1]);
+        lgkm_pin<2>(r);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          dv[d] = O::mma(tr_frag<E>(r[u], 0), pk[u][0], dv[d]);
+          dv[d] = O::mma(tr_frag<E>(r[u], 1), pk[u][1], dv[d]);
+        }
+      }
+      // ---- dK_i^T += Q_i^T dS_i (transposed Q_i reads)
+#pragma unroll
+      for (int i = 0; i < N; ++i)
+#pragma unroll
+        for (int d = 0; d < NHB; ++d) {
+          lds64 r[2][4];
+          tr_issue<QI::ROWB, 0>(r[0], sa0 + i * QB + tq[d][0], sa0 + i * QB + tq[d][1]);
+          tr_issue<QI::ROWB, 32>(r[1], sa0 + i * QB + tq[d][0], sa0 + i * QB + tq[d][1]);
+          lgkm_pin<2>(r);
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            dk[i][d] = O::mma(tr_frag<E>(r[u], 0), ds[u][i][0], dk[i][d]);
+            dk[i][d] = O::mma(tr_frag<E>(r[u], 1), ds[u][i][1], dk[i][d]);
+          }
+        }
+    }
+    pin_acc();
+    wait_vm(mypieces * max(0, min(NS - 2, ntiles - 2 - t)));
+    lds_barrier();
+  };
+  const int thead = min(ntiles, (BK - 2) / BQ + 1);                    // q0 < kb0 + BK - 1
+  const int ttail = max(thead, ntiles - ((T - kb0) % BQ != 0 ? 1 : 0));  // q0 + BQ > T
+  for (int t = 0; t < thead; ++t) step(t, std::true_type{});
+  for (int t = thead; t < ttail; ++t) step(t, std::false_type{});
+  for (int t = ttail; t < ntiles; ++t) step(t, std::true_type{});
+
+  if (!wave_keys || krow >= T) return;
+  E* gdk = reinterpret_cast<E*>(p.dk.p) + b * p.dk.sb + (int64_t)krow * p.dk.st + hh * p.dk.sh;
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+#pragma unroll
+    for (int d = 0; d < NHB; ++d)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int e = d * 32 + 8 * g + 4 * hf;
+        store4<E>(gdk + i * p.dk.si + e, dk[i][d][4 * g] * p.scale, dk[i][d][4 * g + 1] * p.scale,
+                  dk[i][d][4 * g + 2] * p.scale, dk[i][d][4 * g + 3] * p.scale);
+      }
+  E* gdv = reinterpret_cast<E*>(p.dv.p) + b * p.dv.sb + (int64_t)krow * p.dv.st + hh * p.dv.sh;
+#pragma unroll
+  for (int d = 0; d < NVB; ++d)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int e = d * 32 + 8 * g + 4 * hf;
+      store4<E>(gdv + e, dv[d][4 * g], dv[d][4 * g + 1], dv[d][4 * g + 2], dv[d][4 * g + 3]);
+    }
+}
+
+// dK/dV kernel choice for A/B measurements: unset / DTA_DKDV=8 the 8-wave kernel
+// with descriptor staging, DTA_DKDV=4 the one-wave-per-SIMD kernel where its plan
+// fits, DTA_DKDV=0 the 8-wave kernel with address-computed staging.
+inline int dkdv_mode() {
+  static const int m = [] {
+    const char* s = getenv("DTA_DKDV");
+    return s && s[0] == '4' ? 4 : (s && s[0] == '0' ? 0 : 8);
+  }();
+  return m;
+}
+
 // ------------------------------------------------------------ launchers ---
 template <class K>
 static inline int set_smem(K kernel, int bytes) {
@@ -1173,21 +1543,40 @@ template <class E, int HS, int N>
 int launch_dkdv_t(const BwdParams& p, hipStream_t st) {
   using PL = Plan<E, HS, N>;
   constexpr int NW = PL::KVW, DV = PL::DV;
+  if constexpr (Dkdv4Cfg<E, HS, N, DV>::ok) {
+    if (dkdv_mode() == 4 && ring_layout_ok(p, (int)sizeof(E))) {
+      using C4 = Dkdv4Cfg<E, HS, N, DV>;
+      auto kern = attn_dkdv4_kernel<E, HS, N, DV>;
+      if (int e = set_smem(kern, C4::bytes)) return e;
+      hipLaunchKernelGGL(kern, dim3((p.T + C4::BK - 1) / C4::BK, p.H, p.B), dim3(C4::NW * 64), C4::bytes, st, p);
+      return (int)hipGetLastError();
+    }
+  }
   constexpr int bytes = DkdvCfg<E, HS, N, DV, NW>::bytes;
   dim3 grid((p.T + NW * 32 - 1) / (NW * 32), p.H, p.B);
   dim3 block(NW * 64);
-  if constexpr (DkdvSplit<HS, N, DV>::fused) {
-    auto kern = attn_dkdv_kernel<E, HS, N, DV, NW, true, true>;
+  constexpr bool FUSED = DkdvSplit<HS, N, DV>::fused;
+  auto run = [&](auto DKV, auto DVVV, auto SRDV) -> int {
+    auto kern = attn_dkdv_kernel<E, HS, N, DV, NW, decltype(DKV)::value, decltype(DVVV)::value, decltype(SRDV)::value>;
     if (int e = set_smem(kern, bytes)) return e;
     hipLaunchKernelGGL(kern, grid, block, bytes, st, p);
+    return 0;
+  };
+  auto go = [&](auto SRDV) -> int {
+    if constexpr (FUSED) {
+      return run(std::true_type{}, std::true_type{}, SRDV);
+    } else {
+      if (int e = run(std::true_type{}, std::false_type{}, SRDV)) return e;
+      return run(std::false_type{}, std::true_type{}, SRDV);
+    }
+  };
+  int e = 0;
+  if constexpr (TileRing<E, HS, N, DV, NW, true>::ok) {
+    e = dkdv_mode() != 0 && ring_layout_ok(p, (int)sizeof(E)) ? go(std::true_type{}) : go(std::false_type{});
   } else {
-    auto k1 = attn_dkdv_kernel<E, HS, N, DV, NW, true, false>;
-    auto k2 = attn_dkdv_kernel<E, HS, N, DV, NW, false, true>;
-    if (int e = set_smem(k1, bytes)) return e;
-    if (int e = set_smem(k2, bytes)) return e;
-    hipLaunchKernelGGL(k1, grid, block, bytes, st, p);
-    hipLaunchKernelGGL(k2, grid, block, bytes, st, p);
+    e = go(std::false_type{});
   }
+  if (e) return e;
   return (int)hipGetLastError();
 }
 

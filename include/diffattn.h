@@ -26,7 +26,7 @@
  *   Q, K   [b][t][h][i][d]   i < n_terms (the N softmax branches), d < head_size
  *   V, O   [b][t][h][e]      e < dv (dv = 2*head_size for diff attention)
  *   Obr    [i][b][t][h][e]   per-branch normalised outputs A_i V (saved for bwd)
- *   LSE    [i][b][h][t]      fp32, log2-sum-exp of the scaled scores
+ *   LSE    [i][b][h][t]      fp32, NEGATED log2-sum-exp of the scaled scores (-log2 sum 2^(s*scale*log2e))
  *   coef   [h][i]            fp32, signed branch weights (diff: [1, -lambda];
  *                            N-diff: [+l0, -l1, +l2, ...])
  */
