@@ -251,6 +251,77 @@ constexpr int ring_stages(int fixed_bytes, int tile_bytes) {
   return (fixed_bytes + 4 * tile_bytes <= 160 * 1024) ? 4 : (fixed_bytes + 3 * tile_bytes <= 160 * 1024) ? 3 : 2;
 }
 
+// one LDS-DMA piece: SZ bytes per lane from byte voff of the buffer [base, base + bytes)
+// (zeros past its end) to lds + SZ * lane.  base, bytes and lds are wave-uniform.
+// (The transfer size is a literal in each helper: the host pass of hipcc rejects
+// a template-dependent size here.)
+__device__ __forceinline__ void buf_lds16(const void* base, uint32_t bytes, char* lds, uint32_t voff) {
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)lds, 16, voff, 0, 0, 0);
+}
+__device__ __forceinline__ void buf_lds4(const void* base, uint32_t bytes, char* lds, uint32_t voff) {
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)lds, 4, voff, 0, 0, 0);
+}
+
+// One key tile of the query-major kernels -- K_i rows ([N][BN][HS] image) and V
+// rows ([BN][DVC] image, columns from the V base given) -- by buffer_load ... lds
+// with per-tile descriptors; rows past T read as zeros (masked as keys >= T).
+// Wave w issues pieces u * NW + w; single-kind slots resolve at compile time.
+template <class E, int HS, int N, int DVC, int BN, int NW>
+struct KvRing {
+  static constexpr int ES = (int)sizeof(E);
+  static constexpr int KB = BN * HS * ES, VB = BN * DVC * ES;
+  static constexpr int PK = N * KB / 1024, PV = VB / 1024, NPC = PK + PV;
+  static constexpr int MYP = (NPC + NW - 1) / NW;
+  static constexpr bool ok = ES == 2 && HS >= 32 && KB % 1024 == 0 && VB % 1024 == 0;
+
+  __device__ static int pieces(int wave) { return NPC / NW + (wave < NPC % NW ? 1 : 0); }
+  __device__ static uint32_t offk(int64_t st, int64_t si, int j, int lane) {
+    using KI = Img<E, HS>;
+    const int i = j / (KB / 1024), pb = (j % (KB / 1024)) * 1024 + lane * 16;
+    const int r = pb / KI::ROWB, c = ((pb % KI::ROWB) >> 4) ^ swz<KI::ROWB>(r);
+    return (uint32_t)(r * (uint32_t)(st * ES) + (uint32_t)(i * si * ES) + c * 16);
+  }
+  __device__ static uint32_t offv(int64_t st, int j, int lane) {
+    using VI = Img<E, DVC>;
+    const int pb = (j - PK) * 1024 + lane * 16;
+    const int r = pb / VI::ROWB, c = ((pb % VI::ROWB) >> 4) ^ swz<VI::ROWB>(r);
+    return (uint32_t)(r * (uint32_t)(st * ES) + c * 16);
+  }
+  __device__ static void issue(const E* gk, int64_t kst, int64_t ksi, const E* gv, int64_t vst, int k0, int T,
+                               E* kdst, E* vdst, int wave, int lane) {
+    const int rows = T - k0;
+    const E* bk = gk + (int64_t)k0 * kst;
+    const E* bv = gv + (int64_t)k0 * vst;
+    const uint32_t nk = (uint32_t)rows * (uint32_t)(kst * ES), nv = (uint32_t)rows * (uint32_t)(vst * ES);
+    char* kd = reinterpret_cast<char*>(kdst);
+    char* vd = reinterpret_cast<char*>(vdst);
+    sfor<MYP>([&](auto U) {
+      constexpr int u = decltype(U)::value;
+      const int j = u * NW + wave;
+      if constexpr ((u + 1) * NW <= PK) {
+        buf_lds16(bk, nk, kd + j * 1024, offk(kst, ksi, j, lane));
+      } else if constexpr (u * NW >= PK && (u + 1) * NW <= NPC) {
+        buf_lds16(bv, nv, vd + (j - PK) * 1024, offv(vst, j, lane));
+      } else {
+        if (j < PK) buf_lds16(bk, nk, kd + j * 1024, offk(kst, ksi, j, lane));
+        else if (j < NPC) buf_lds16(bv, nv, vd + (j - PK) * 1024, offv(vst, j, lane));
+      }
+    });
+  }
+};
+
+// K/V descriptors cover [row base, T rows): every branch's K columns inside one
+// row stride, V's DV columns too, extents within the 32-bit record count.
+template <class P>
+inline bool kv_layout_ok(const P& p, int es) {
+  const int64_t ks = p.k.st, vs = p.v.st;
+  if (ks <= 0 || vs <= 0 || p.k.si < 0) return false;
+  if ((int64_t)(p.N - 1) * p.k.si + p.HS > ks || p.DV > vs) return false;
+  return (int64_t)p.T * ks * es < (1ll << 31) && (int64_t)p.T * vs * es < (1ll << 31);
+}
+
 // ---------------------------------------------------------------- forward ---
 template <class E> struct FwdTile { static constexpr int BN = 64; };
 template <> struct FwdTile<float> { static constexpr int BN = 32; };
@@ -292,7 +363,7 @@ struct FwdPick {
   static constexpr bool ok = FwdCfg<E, HS, N, DVC, NW, QREG>::bytes <= LIM;
 };
 
-template <class E, int HS, int N, int DVC, int NW, bool QREG>
+template <class E, int HS, int N, int DVC, int NW, bool QREG, bool SRD>
 __global__ __launch_bounds__(NW * 64, (FwdCfg<E, HS, N, DVC, NW, QREG>::WPE)) void attn_fwd_kernel(FwdParams p) {
   using O = Ops<E>;
   using frag = typename O::frag;
@@ -353,14 +424,20 @@ __global__ __launch_bounds__(NW * 64, (FwdCfg<E, HS, N, DVC, NW, QREG>::WPE)) vo
 
   const int kend = min(T, q0 + BM);
   const int ntiles = (kend + BN - 1) / BN;
+  using KR = KvRing<E, HS, N, DVC, BN, NW>;
   auto stage_kv = [&](int kt, int buf) {
     const int k0 = kt * BN;
+    if constexpr (SRD) {
+      KR::issue(gk, p.k.st, p.k.si, gv, p.v.st, k0, T, Kb + buf * N * BN * HS, Vb + buf * BN * DVC, wave, lane);
+    } else {
 #pragma unroll
-    for (int i = 0; i < N; ++i)
-      stage<E, HS, BN, HS, NTHR>(Kb + (buf * N + i) * BN * HS, gk + i * p.k.si, p.k.st, k0, T - 1, tid);
-    stage<E, DVC, BN, DVC, NTHR>(Vb + buf * BN * DVC, gv, p.v.st, k0, T - 1, tid);
+      for (int i = 0; i < N; ++i)
+        stage<E, HS, BN, HS, NTHR>(Kb + (buf * N + i) * BN * HS, gk + i * p.k.si, p.k.st, k0, T - 1, tid);
+      stage<E, DVC, BN, DVC, NTHR>(Vb + buf * BN * DVC, gv, p.v.st, k0, T - 1, tid);
+    }
   };
-  const int tile_pieces = N * stage_pieces<E, HS, BN, HS, NW>(wave) + stage_pieces<E, DVC, BN, DVC, NW>(wave);
+  const int tile_pieces = SRD ? KR::pieces(wave)
+                              : N * stage_pieces<E, HS, BN, HS, NW>(wave) + stage_pieces<E, DVC, BN, DVC, NW>(wave);
   for (int j = 0; j < NS - 1; ++j)
     if (j < ntiles) stage_kv(j, j);
   wait_vm(tile_pieces * max(0, min(NS - 1, ntiles) - 1));   // tile 0 (and the Q block) landed
@@ -587,7 +664,7 @@ struct DqPick {
   static constexpr bool ok = DqCfg<E, HS, N, 2 * HS, NW, QREG>::bytes <= LIM;
 };
 
-template <class E, int HS, int N, int DV, int NW, bool QREG, bool OUTF32>
+template <class E, int HS, int N, int DV, int NW, bool QREG, bool OUTF32, bool SRD>
 __global__ __launch_bounds__(NW * 64, simd_waves(NW, DqCfg<E, HS, N, DV, NW, QREG>::bytes))
 void attn_dq_kernel(BwdParams p) {
   using O = Ops<E>;
@@ -631,12 +708,18 @@ void attn_dq_kernel(BwdParams p) {
 
   const int kend = min(T, q0 + BM);
   const int ntiles = (kend + BN - 1) / BN;
+  using KR = KvRing<E, HS, N, DV, BN, NW>;
+  static_assert(!SRD || HSP == HS, "descriptor staging needs unpadded K rows");
   auto stage_kv = [&](int kt, int buf) {
     const int k0 = kt * BN;
+    if constexpr (SRD) {
+      KR::issue(gk, p.k.st, p.k.si, gv, p.v.st, k0, T, Kb + buf * N * BN * HSP, Vb + buf * BN * DV, wave, lane);
+    } else {
 #pragma unroll
-    for (int i = 0; i < N; ++i)
-      stage<E, HSP, BN, HS, NTHR>(Kb + (buf * N + i) * BN * HSP, gk + i * p.k.si, p.k.st, k0, T - 1, tid);
-    stage<E, DV, BN, DV, NTHR>(Vb + buf * BN * DV, gv, p.v.st, k0, T - 1, tid);
+      for (int i = 0; i < N; ++i)
+        stage<E, HSP, BN, HS, NTHR>(Kb + (buf * N + i) * BN * HSP, gk + i * p.k.si, p.k.st, k0, T - 1, tid);
+      stage<E, DV, BN, DV, NTHR>(Vb + buf * BN * DV, gv, p.v.st, k0, T - 1, tid);
+    }
   };
 
   // ---- per-row operands in registers: Q_i and dO rows (B operands), LSE, delta
@@ -685,7 +768,8 @@ void attn_dq_kernel(BwdParams p) {
 #pragma unroll
     for (int i = 0; i < N; ++i) stage<E, HS, BM, HS, NTHR>(Qs + i * BM * HS, gq + i * p.q.si, p.q.st, q0, T - 1, tid);
   }
-  const int tile_pieces = N * stage_pieces<E, HSP, BN, HS, NW>(wave) + stage_pieces<E, DV, BN, DV, NW>(wave);
+  const int tile_pieces = SRD ? KR::pieces(wave)
+                              : N * stage_pieces<E, HSP, BN, HS, NW>(wave) + stage_pieces<E, DV, BN, DV, NW>(wave);
   for (int j = 0; j < NS - 1; ++j)
     if (j < ntiles) stage_kv(j, j);
   wait_vm(tile_pieces * max(0, min(NS - 1, ntiles) - 1));
@@ -831,19 +915,6 @@ void attn_dq_kernel(BwdParams p) {
           store4<E>(gdq + e, a0, a1, a2, a3);
         }
       }
-}
-
-// one LDS-DMA piece: SZ bytes per lane from byte voff of the buffer [base, base + bytes)
-// (zeros past its end) to lds + SZ * lane.  base, bytes and lds are wave-uniform.
-// (The transfer size is a literal in each helper: the host pass of hipcc rejects
-// a template-dependent size here.)
-__device__ __forceinline__ void buf_lds16(const void* base, uint32_t bytes, char* lds, uint32_t voff) {
-  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)lds, 16, voff, 0, 0, 0);
-}
-__device__ __forceinline__ void buf_lds4(const void* base, uint32_t bytes, char* lds, uint32_t voff) {
-  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)lds, 4, voff, 0, 0, 0);
 }
 
 // One query tile of the key-major backward -- Q_i rows, dO rows, LSE rows and
@@ -1482,6 +1553,16 @@ __global__ __launch_bounds__(256, 1) void attn_dkdv4_kernel(BwdParams p) {
 // dK/dV kernel choice for A/B measurements: unset / DTA_DKDV=8 the 8-wave kernel
 // with descriptor staging, DTA_DKDV=4 the one-wave-per-SIMD kernel where its plan
 // fits, DTA_DKDV=0 the 8-wave kernel with address-computed staging.
+// DTA_KV_STAGING=0: forward / dQ kernels stage K and V by per-lane addresses
+// instead of buffer descriptors (A/B measurements)
+inline bool kv_staging() {
+  static const bool on = [] {
+    const char* s = getenv("DTA_KV_STAGING");
+    return !(s && s[0] == '0');
+  }();
+  return on;
+}
+
 inline int dkdv_mode() {
   static const int m = [] {
     const char* s = getenv("DTA_DKDV");
@@ -1513,10 +1594,19 @@ int launch_fwd_t(const FwdParams& p, hipStream_t st) {
   using FP = typename PL::FP;
   constexpr int DVC = FP::DVC, NW = FP::NW;
   constexpr int bytes = FwdCfg<E, HS, N, DVC, NW, FP::QREG>::bytes;
-  auto kern = attn_fwd_kernel<E, HS, N, DVC, NW, FP::QREG>;
-  if (int e = set_smem(kern, bytes)) return e;
   dim3 grid((p.T + NW * 32 - 1) / (NW * 32), p.H * (PL::DV / DVC), p.B);
-  hipLaunchKernelGGL(kern, grid, dim3(NW * 64), bytes, st, p);
+  auto run = [&](auto SRDV) -> int {
+    auto kern = attn_fwd_kernel<E, HS, N, DVC, NW, FP::QREG, decltype(SRDV)::value>;
+    if (int e = set_smem(kern, bytes)) return e;
+    hipLaunchKernelGGL(kern, grid, dim3(NW * 64), bytes, st, p);
+    return 0;
+  };
+  int e = 0;
+  if constexpr (KvRing<E, HS, N, DVC, FwdCfg<E, HS, N, DVC, NW, FP::QREG>::BN, NW>::ok)
+    e = kv_staging() && kv_layout_ok(p, (int)sizeof(E)) ? run(std::true_type{}) : run(std::false_type{});
+  else
+    e = run(std::false_type{});
+  if (e) return e;
   return (int)hipGetLastError();
 }
 
@@ -1527,15 +1617,19 @@ int launch_dq_t(const BwdParams& p, hipStream_t st) {
   constexpr bool QR = PL::DP::QREG;
   constexpr int bytes = DqCfg<E, HS, N, DV, NW, QR>::bytes;
   dim3 grid((p.T + NW * 32 - 1) / (NW * 32), p.H, p.B);
-  if (p.dq32) {
-    auto kern = attn_dq_kernel<E, HS, N, DV, NW, QR, true>;
+  auto run = [&](auto F32, auto SRDV) -> int {
+    auto kern = attn_dq_kernel<E, HS, N, DV, NW, QR, decltype(F32)::value, decltype(SRDV)::value>;
     if (int e = set_smem(kern, bytes)) return e;
     hipLaunchKernelGGL(kern, grid, dim3(NW * 64), bytes, st, p);
-  } else {
-    auto kern = attn_dq_kernel<E, HS, N, DV, NW, QR, false>;
-    if (int e = set_smem(kern, bytes)) return e;
-    hipLaunchKernelGGL(kern, grid, dim3(NW * 64), bytes, st, p);
-  }
+    return 0;
+  };
+  auto go = [&](auto SRDV) -> int { return p.dq32 ? run(std::true_type{}, SRDV) : run(std::false_type{}, SRDV); };
+  int e = 0;
+  if constexpr (KvRing<E, HS, N, DV, DqCfg<E, HS, N, DV, NW, QR>::BN, NW>::ok && DqCfg<E, HS, N, DV, NW, QR>::HSP == HS)
+    e = kv_staging() && kv_layout_ok(p, (int)sizeof(E)) ? go(std::true_type{}) : go(std::false_type{});
+  else
+    e = go(std::false_type{});
+  if (e) return e;
   return (int)hipGetLastError();
 }
 

@@ -1,7 +1,7 @@
 # Per-kernel VGPR / scratch / occupancy of the attention kernels (cross-compiled, no GPU).
 cd $(dirname $0)/../differential_transformer_replication_amd/csrc
 for f in ${@:-attn_bf16 attn_f16 attn_f32}; do
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -munsafe-fp-atomics -fno-honor-nans \
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -munsafe-fp-atomics -fno-honor-nans -fno-slp-vectorize \
     -Rpass-analysis=kernel-resource-usage -c $f.hip -o /dev/null 2>&1 | python3 -c "
 import sys, re
 name = None; row = {}
