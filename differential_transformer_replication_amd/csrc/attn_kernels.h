@@ -453,6 +453,8 @@ __global__ __launch_bounds__(NW * 64, (FwdCfg<E, HS, N, DVC, NW, QREG>::WPE)) vo
     for (int d = 0; d < NDB; ++d) acc[i][d] = f32x16{};
   }
   const bool wave_live = qw0 < T;
+  // static priority for the second-dispatched half (MI355X_MICROARCH.md, two waves per SIMD, item 4)
+  if (NW == 8 && p.prio && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
 
   // two loops over straight-line bodies: tiles strictly below the block's first
   // query row and inside T need no mask; the block's diagonal / tail tiles do
@@ -781,6 +783,8 @@ void attn_dq_kernel(BwdParams p) {
 #pragma unroll
     for (int d = 0; d < NHB; ++d) dq[i][d] = f32x16{};
   const bool wave_live = qw0 < T;
+  // static priority for the second-dispatched half (MI355X_MICROARCH.md, two waves per SIMD, item 4)
+  if (NW == 8 && p.prio && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
 
   // unmasked loop, then the block's diagonal / tail tiles (see attn_fwd_kernel)
   auto step = [&](int kt, auto MASKED) {
@@ -1119,6 +1123,8 @@ __global__ __launch_bounds__(NW * 64, (NW >= 8 ? 2 : 1)) void attn_dkdv_kernel(B
   wait_vm(tile_pieces * max(0, min(NS - 1, ntiles) - 1));
   lds_barrier();
   const bool wave_keys = kw0 < T;
+  // static priority for the second-dispatched half (MI355X_MICROARCH.md, two waves per SIMD, item 4)
+  if (NW == 8 && p.prio && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
 
   // masked diagonal tiles, unmasked interior, masked ragged tail tile; each loop
   // is one straight-line body (both variants behind a branch spill).  Lanes with

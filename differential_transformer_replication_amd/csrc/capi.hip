@@ -89,6 +89,16 @@ bool ok_dims(int dtype, int B, int T, int H, int N, int hs, int dv) {
 
 }  // namespace
 
+// DTA_PRIO=1 gives the second wave half of 8-wave workgroups a static s_setprio 1
+// (A/B measurements; default off)
+static int wave_prio() {
+  static const int v = [] {
+    const char* e = getenv("DTA_PRIO");
+    return e && e[0] == '1' ? 1 : 0;
+  }();
+  return v;
+}
+
 extern "C" {
 
 int dta_abi_version(void) { return DTA_ABI_VERSION; }
@@ -122,6 +132,7 @@ int dta_attn_fwd(const dta_attn_fwd_args* a, void* stream) {
   p.lse = a->lse; p.coef = a->coef;
   p.B = a->B; p.T = a->T; p.H = a->H; p.N = a->n_terms; p.HS = a->head_size; p.DV = a->dv;
   p.sl2 = a->scale * kLog2e;
+  p.prio = wave_prio();
   return status(launch_attn_fwd(a->dtype, p, (hipStream_t)stream));
 }
 
@@ -156,6 +167,7 @@ int dta_attn_bwd(const dta_attn_bwd_args* a, void* stream) {
   p.dq32 = a->dq.ptr ? nullptr : a->dq_f32;
   p.B = a->B; p.T = a->T; p.H = a->H; p.N = a->n_terms; p.HS = a->head_size; p.DV = a->dv;
   p.scale = a->scale; p.sl2 = a->scale * kLog2e;
+  p.prio = wave_prio();
   int e = 0;
   if ((stages & DTA_BWD_DQ) && (e = launch_attn_dq(a->dtype, p, st))) return status(e);
   if ((stages & DTA_BWD_DKDV) && (e = launch_attn_dkdv(a->dtype, p, st))) return status(e);

@@ -17,6 +17,7 @@ struct FwdParams {
   const float* coef;
   int B, T, H, N, HS, DV;
   float sl2;           // scale * log2(e)
+  int prio;            // 1: waves 4-7 of an 8-wave workgroup run at s_setprio 1
 };
 
 struct BwdParams {
@@ -28,6 +29,7 @@ struct BwdParams {
   float* dq32;         // if set: dQ written as fp32 [b][t][h][i][d] instead of into dq
   int B, T, H, N, HS, DV;
   float sl2, scale;
+  int prio;            // as FwdParams::prio
 };
 
 // per-dtype launchers (dtype index: 0 bf16, 1 f16, 2 f32); return hipError_t
