@@ -141,6 +141,33 @@ def control_bench(B, H, hs, T, steps, warmup):
     return sec * 1e3, f / sec / 1e12
 
 
+def control_fused_bench(B, H, hs, T, steps, warmup):
+    """The same control attention on this repo's fused kernels (N=1, coef 1, dv=hs):
+    the like-for-like comparison of BASELINE configs[4].  Returns (ms, TFLOP/s)."""
+    from differential_transformer_replication_amd import ops
+    dev = torch.device("cuda", torch.cuda.current_device())
+    g = torch.Generator(device=dev).manual_seed(7)
+    W = ops.packed_width(H, 1, hs, hs)
+    qkv = torch.randn(B, T, W, device=dev, dtype=torch.bfloat16, generator=g).requires_grad_(True)
+    do = torch.randn(B, T, H * hs, device=dev, dtype=torch.bfloat16, generator=g)
+    coef = torch.ones(H, 1, device=dev, dtype=torch.float32)
+
+    def step():
+        qkv.grad = None
+        ops.diff_attention(qkv, coef, H, 1, hs, dv=hs).backward(do)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    sec = (time.perf_counter() - t0) / steps
+    f = 3.0 * B * H * T * T * (hs + hs)
+    return sec * 1e3, f / sec / 1e12
+
+
 def kernel_bench(args, world, rank):
     from differential_transformer_replication_amd import ops
     from differential_transformer_replication_amd.diff_transformer import _layer_lambda_coef
@@ -213,11 +240,17 @@ def kernel_bench(args, world, rank):
     }
     if args.control and rank == 0:
         # control.py standard attention at equal F_fwd: 2*H heads of width hs, dv = hs (train.py:226)
-        cms, ctf = control_bench(B, 2 * H if N == 2 else H, hs, T, args.steps, args.warmup)
-        res["control"] = {"what": "control.py causal softmax attention, torch SDPA (ROCm fused attention), bf16 fwd+bwd, "
-                                  f"B={B} H={2 * H if N == 2 else H} hs=dv={hs} T={T}",
-                          "ms_per_step": round(cms, 4), "alg_tflops": round(ctf, 2),
-                          "diff_over_control_time": round(ms / cms, 3)}
+        Hc = 2 * H if N == 2 else H
+        cms, ctf = control_bench(B, Hc, hs, T, args.steps, args.warmup)
+        fms, ftf = control_fused_bench(B, Hc, hs, T, args.steps, args.warmup)
+        res["control"] = {"what": "control.py causal softmax attention (control.py:38-63), bf16 fwd+bwd, "
+                                  f"B={B} H={Hc} hs=dv={hs} T={T}",
+                          "same_kernel": {"how": "this repo's fused kernels, N=1, coef 1, dv=hs (SURVEY 8f item 2)",
+                                          "ms_per_step": round(fms, 4), "alg_tflops": round(ftf, 2),
+                                          "diff_over_control_time": round(ms / fms, 3)},
+                          "torch_sdpa": {"how": "torch scaled_dot_product_attention (ROCm fused attention)",
+                                         "ms_per_step": round(cms, 4), "alg_tflops": round(ctf, 2),
+                                         "diff_over_control_time": round(ms / cms, 3)}}
     return res
 
 

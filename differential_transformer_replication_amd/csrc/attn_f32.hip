@@ -5,5 +5,5 @@ namespace dta {
 int launch_attn_fwd_f32(const FwdParams& p, hipStream_t st) { return dispatch_fwd<float>(p, st); }
 int launch_attn_dq_f32(const BwdParams& p, hipStream_t st) { return dispatch_dq<float>(p, st); }
 int launch_attn_dkdv_f32(const BwdParams& p, hipStream_t st) { return dispatch_dkdv<float>(p, st); }
-bool attn_supported_f32(int hs, int n) { return supported_t<float>(hs, n); }
+bool attn_supported_f32(int hs, int n, int dv) { return supported_t<float>(hs, n, dv); }
 }  // namespace dta

@@ -348,9 +348,9 @@ struct FwdCfg {
   static constexpr int WPE = regs <= 256 ? 2 : simd_waves(NW, bytes);
 };
 
-template <class E, int HS, int N>
+template <class E, int HS, int N, int DV = 2 * HS>
 struct FwdPick {
-  static constexpr int DVC = FwdChunk<N, 2 * HS>::DVC;
+  static constexpr int DVC = FwdChunk<N, DV>::DVC;
   static constexpr int LIM = 160 * 1024;
   static constexpr int NWMAX = sizeof(E) == 2 ? 8 : 4;
   // widest workgroup with Q in LDS, else Q in registers
@@ -657,13 +657,13 @@ struct DqCfg {
   static constexpr int bytes = (nQ + NS * nK + NS * nV) * (int)sizeof(E);
 };
 
-template <class E, int HS, int N>
+template <class E, int HS, int N, int DV = 2 * HS>
 struct DqPick {
   static constexpr int LIM = 160 * 1024;
-  static constexpr bool q8 = sizeof(E) == 2 && DqCfg<E, HS, N, 2 * HS, 8, false>::bytes <= LIM;
+  static constexpr bool q8 = sizeof(E) == 2 && DqCfg<E, HS, N, DV, 8, false>::bytes <= LIM;
   static constexpr int NW = q8 ? 8 : (sizeof(E) == 2 ? 4 : 2);
   static constexpr bool QREG = !q8;
-  static constexpr bool ok = DqCfg<E, HS, N, 2 * HS, NW, QREG>::bytes <= LIM;
+  static constexpr bool ok = DqCfg<E, HS, N, DV, NW, QREG>::bytes <= LIM;
 };
 
 template <class E, int HS, int N, int DV, int NW, bool QREG, bool OUTF32, bool SRD>
@@ -1585,18 +1585,18 @@ static inline int set_smem(K kernel, int bytes) {
   return 0;
 }
 
-template <class E, int HS, int N>
+template <class E, int HS, int N, int DV_ = 2 * HS>
 struct Plan {
-  static constexpr int DV = 2 * HS;
-  using FP = FwdPick<E, HS, N>;
-  using DP = DqPick<E, HS, N>;
+  static constexpr int DV = DV_;
+  using FP = FwdPick<E, HS, N, DV>;
+  using DP = DqPick<E, HS, N, DV>;
   static constexpr int KVW = DkdvWaves<E, HS, N, DV>::v;
   static constexpr bool ok = FP::ok && DP::ok && DkdvCfg<E, HS, N, DV, KVW>::bytes <= 160 * 1024;
 };
 
-template <class E, int HS, int N>
+template <class E, int HS, int N, int DV_>
 int launch_fwd_t(const FwdParams& p, hipStream_t st) {
-  using PL = Plan<E, HS, N>;
+  using PL = Plan<E, HS, N, DV_>;
   using FP = typename PL::FP;
   constexpr int DVC = FP::DVC, NW = FP::NW;
   constexpr int bytes = FwdCfg<E, HS, N, DVC, NW, FP::QREG>::bytes;
@@ -1616,9 +1616,9 @@ int launch_fwd_t(const FwdParams& p, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
-template <class E, int HS, int N>
+template <class E, int HS, int N, int DV_>
 int launch_dq_t(const BwdParams& p, hipStream_t st) {
-  using PL = Plan<E, HS, N>;
+  using PL = Plan<E, HS, N, DV_>;
   constexpr int NW = PL::DP::NW, DV = PL::DV;
   constexpr bool QR = PL::DP::QREG;
   constexpr int bytes = DqCfg<E, HS, N, DV, NW, QR>::bytes;
@@ -1639,9 +1639,9 @@ int launch_dq_t(const BwdParams& p, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
-template <class E, int HS, int N>
+template <class E, int HS, int N, int DV_>
 int launch_dkdv_t(const BwdParams& p, hipStream_t st) {
-  using PL = Plan<E, HS, N>;
+  using PL = Plan<E, HS, N, DV_>;
   constexpr int NW = PL::KVW, DV = PL::DV;
   if constexpr (Dkdv4Cfg<E, HS, N, DV>::ok) {
     if (dkdv_mode() == 4 && ring_layout_ok(p, (int)sizeof(E))) {
@@ -1680,14 +1680,18 @@ int launch_dkdv_t(const BwdParams& p, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
+// (head size, branches, value width): the differential models' dv = 2 hs, plus the
+// control model's standard attention (N = 1, dv = hs; control.py:38-63)
 #define DTA_FOR_CONFIGS(X) \
-  X(16, 1) X(16, 2) X(16, 3) X(16, 4) X(32, 1) X(32, 2) X(32, 3) X(32, 4) \
-  X(64, 1) X(64, 2) X(64, 3) X(64, 4) X(128, 1) X(128, 2) X(128, 3) X(128, 4)
+  X(16, 1, 32) X(16, 2, 32) X(16, 3, 32) X(16, 4, 32) X(32, 1, 64) X(32, 2, 64) X(32, 3, 64) X(32, 4, 64) \
+  X(64, 1, 128) X(64, 2, 128) X(64, 3, 128) X(64, 4, 128) X(128, 1, 256) X(128, 2, 256) X(128, 3, 256) \
+  X(128, 4, 256) X(64, 1, 64) X(128, 1, 128)
 
 template <class E>
 int dispatch_fwd(const FwdParams& p, hipStream_t st) {
-#define DTA_F(HS_, N_) \
-  if (p.HS == HS_ && p.N == N_) { if constexpr (Plan<E, HS_, N_>::ok) return launch_fwd_t<E, HS_, N_>(p, st); else return -2; }
+#define DTA_F(HS_, N_, DV_) \
+  if (p.HS == HS_ && p.N == N_ && p.DV == DV_) { \
+    if constexpr (Plan<E, HS_, N_, DV_>::ok) return launch_fwd_t<E, HS_, N_, DV_>(p, st); else return -2; }
   DTA_FOR_CONFIGS(DTA_F)
 #undef DTA_F
   return -2;
@@ -1695,8 +1699,9 @@ int dispatch_fwd(const FwdParams& p, hipStream_t st) {
 
 template <class E>
 int dispatch_dq(const BwdParams& p, hipStream_t st) {
-#define DTA_Q(HS_, N_) \
-  if (p.HS == HS_ && p.N == N_) { if constexpr (Plan<E, HS_, N_>::ok) return launch_dq_t<E, HS_, N_>(p, st); else return -2; }
+#define DTA_Q(HS_, N_, DV_) \
+  if (p.HS == HS_ && p.N == N_ && p.DV == DV_) { \
+    if constexpr (Plan<E, HS_, N_, DV_>::ok) return launch_dq_t<E, HS_, N_, DV_>(p, st); else return -2; }
   DTA_FOR_CONFIGS(DTA_Q)
 #undef DTA_Q
   return -2;
@@ -1704,16 +1709,17 @@ int dispatch_dq(const BwdParams& p, hipStream_t st) {
 
 template <class E>
 int dispatch_dkdv(const BwdParams& p, hipStream_t st) {
-#define DTA_K(HS_, N_) \
-  if (p.HS == HS_ && p.N == N_) { if constexpr (Plan<E, HS_, N_>::ok) return launch_dkdv_t<E, HS_, N_>(p, st); else return -2; }
+#define DTA_K(HS_, N_, DV_) \
+  if (p.HS == HS_ && p.N == N_ && p.DV == DV_) { \
+    if constexpr (Plan<E, HS_, N_, DV_>::ok) return launch_dkdv_t<E, HS_, N_, DV_>(p, st); else return -2; }
   DTA_FOR_CONFIGS(DTA_K)
 #undef DTA_K
   return -2;
 }
 
 template <class E>
-bool supported_t(int hs, int n) {
-#define DTA_S(HS_, N_) if (hs == HS_ && n == N_) return Plan<E, HS_, N_>::ok;
+bool supported_t(int hs, int n, int dv) {
+#define DTA_S(HS_, N_, DV_) if (hs == HS_ && n == N_ && dv == DV_) return Plan<E, HS_, N_, DV_>::ok;
   DTA_FOR_CONFIGS(DTA_S)
 #undef DTA_S
   return false;

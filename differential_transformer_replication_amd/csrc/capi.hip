@@ -14,9 +14,9 @@ int launch_attn_dq_f32(const BwdParams&, hipStream_t);
 int launch_attn_dkdv_bf16(const BwdParams&, hipStream_t);
 int launch_attn_dkdv_f16(const BwdParams&, hipStream_t);
 int launch_attn_dkdv_f32(const BwdParams&, hipStream_t);
-bool attn_supported_bf16(int, int);
-bool attn_supported_f16(int, int);
-bool attn_supported_f32(int, int);
+bool attn_supported_bf16(int, int, int);
+bool attn_supported_f16(int, int, int);
+bool attn_supported_f32(int, int, int);
 
 int launch_attn_fwd(int dtype, const FwdParams& p, hipStream_t st) {
   switch (dtype) {
@@ -43,11 +43,12 @@ int launch_attn_dkdv(int dtype, const BwdParams& p, hipStream_t st) {
   return -2;
 }
 bool attn_supported(int dtype, int hs, int n, int dv) {
-  if (dv != 2 * hs) return false;
+  // dv = 2 hs (differential models) or, for standard attention (N = 1), dv = hs
+  if (dv != 2 * hs && !(n == 1 && dv == hs)) return false;
   switch (dtype) {
-    case DTA_BF16: return attn_supported_bf16(hs, n);
-    case DTA_F16: return attn_supported_f16(hs, n);
-    case DTA_F32: return attn_supported_f32(hs, n);
+    case DTA_BF16: return attn_supported_bf16(hs, n, dv);
+    case DTA_F16: return attn_supported_f16(hs, n, dv);
+    case DTA_F32: return attn_supported_f32(hs, n, dv);
   }
   return false;
 }

@@ -69,6 +69,11 @@ class KernelTimer:
 TIMER = KernelTimer()
 
 
+def supported(dtype: torch.dtype, hs: int, N: int, dv: int) -> bool:
+    """Whether libdiffattn.so has a gfx950 kernel plan for this shape (dta_supported)."""
+    return bool(_lib.load().dta_supported(_lib.dtype_code(dtype), hs, N, dv))
+
+
 def packed_width(H: int, N: int, hs: int, dv: int) -> int:
     return 2 * H * N * hs + H * dv
 
@@ -85,19 +90,18 @@ def split_packed(qkv: Tensor, H: int, N: int, hs: int, dv: int):
 
 class _DiffAttention(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, qkv: Tensor, coef: Tensor, H: int, N: int, hs: int, freqs: Optional[Tensor]):
+    def forward(ctx, qkv: Tensor, coef: Tensor, H: int, N: int, hs: int, freqs: Optional[Tensor], dv: int):
         lib = _lib.load()
         _require_gpu(qkv, coef)
         if qkv.dim() != 3:
             raise RuntimeError("qkv must be (B, T, W)")
         qkv = qkv.contiguous()
         B, T, W = qkv.shape
-        dv = 2 * hs
         if W != packed_width(H, N, hs, dv):
             raise RuntimeError(f"packed width {W} != 2*H*N*hs + H*dv = {packed_width(H, N, hs, dv)}")
         dt = _lib.dtype_code(qkv.dtype)
         if not lib.dta_supported(dt, hs, N, dv):
-            raise RuntimeError(f"no gfx950 kernel for head_size={hs}, n_terms={N}, dtype={qkv.dtype}")
+            raise RuntimeError(f"no gfx950 kernel for head_size={hs}, n_terms={N}, dv={dv}, dtype={qkv.dtype}")
         coef = coef.detach().to(torch.float32).contiguous()
         dev = qkv.device
         stream = _lib.stream_handle(dev)
@@ -167,18 +171,20 @@ class _DiffAttention(torch.autograd.Function):
             _lib.check(lib.dta_rope(ra, stream))
             ra = _lib.RopeArgs(dt, B, T, H, N, hs, 1, 0, _lib.tensor5(dk_rot), _lib.tensor5(dk), freqs.data_ptr())
             _lib.check(lib.dta_rope(ra, stream))
-        return dqkv, dcoef, None, None, None, None
+        return dqkv, dcoef, None, None, None, None, None
 
 
 def diff_attention(qkv: Tensor, coef: Tensor, H: int, N: int, hs: int,
-                   freqs: Optional[Tensor] = None) -> Tensor:
+                   freqs: Optional[Tensor] = None, dv: Optional[int] = None) -> Tensor:
     """O = sum_i coef[h,i] softmax_causal(Q_i K_i^T/sqrt(hs)) V for every head.
 
     ``freqs``: fp32 (T, hs/2, 2) rotary table (view_as_real of freqs_cis[:T]) or None.
+    ``dv``: value width per head; 2*hs for the differential models (default), hs for
+    standard attention (N=1, coef 1: control.py:38-63).
     """
     if freqs is not None:
         freqs = freqs.to(device=qkv.device, dtype=torch.float32).contiguous()
-    return _DiffAttention.apply(qkv, coef, H, N, hs, freqs)
+    return _DiffAttention.apply(qkv, coef, H, N, hs, freqs, 2 * hs if dv is None else dv)
 
 
 class _GroupLNScale(torch.autograd.Function):
