@@ -24,7 +24,8 @@
  * Layouts (element strides are given per tensor so strided views of one
  * packed projection output can be passed without copies):
  *   Q, K   [b][t][h][i][d]   i < n_terms (the N softmax branches), d < head_size
- *   V, O   [b][t][h][e]      e < dv (dv = 2*head_size for diff attention)
+ *   V, O   [b][t][h][e]      e < dv (dv = 2*head_size for diff attention; dv = head_size with n_terms = 1
+ *                             for standard attention, head_size 64 or 128)
  *   Obr    [i][b][t][h][e]   per-branch normalised outputs A_i V (saved for bwd)
  *   LSE    [i][b][h][t]      fp32, NEGATED log2-sum-exp of the scaled scores (-log2 sum 2^(s*scale*log2e))
  *   coef   [h][i]            fp32, signed branch weights (diff: [1, -lambda];
