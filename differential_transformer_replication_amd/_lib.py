@@ -23,7 +23,8 @@ ABI_VERSION = 1
 
 # every symbol include/diffattn.h declares
 EXPORTS = ("dta_attn_fwd", "dta_attn_bwd", "dta_attn_bwd_workspace_bytes", "dta_ln_fwd", "dta_ln_bwd",
-           "dta_rope", "dta_cast_f32", "dta_error_string", "dta_abi_version", "dta_supported")
+           "dta_rope", "dta_cast_f32", "dta_error_string", "dta_abi_version", "dta_supported",
+           "dta_attn_decode", "dta_attn_decode_workspace_bytes")
 
 
 class DtaTensor(ctypes.Structure):
@@ -72,6 +73,14 @@ class RopeArgs(ctypes.Structure):
                 ("src", DtaTensor), ("dst", DtaTensor), ("freqs", ctypes.c_void_p)]
 
 
+class DecodeArgs(ctypes.Structure):
+    _fields_ = [("dtype", ctypes.c_int32), ("B", ctypes.c_int32), ("H", ctypes.c_int32),
+                ("n_terms", ctypes.c_int32), ("head_size", ctypes.c_int32), ("dv", ctypes.c_int32),
+                ("length", ctypes.c_int32), ("t_cap", ctypes.c_int32), ("scale", ctypes.c_float),
+                ("q", DtaTensor), ("k_cache", DtaTensor), ("v_cache", DtaTensor), ("o", DtaTensor),
+                ("coef", ctypes.c_void_p), ("workspace", ctypes.c_void_p)]
+
+
 _lock = threading.Lock()
 _lib: Optional[ctypes.CDLL] = None
 
@@ -93,12 +102,15 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         lib.dta_ln_bwd.argtypes = [P(LnArgs), ctypes.c_void_p]
         lib.dta_rope.argtypes = [P(RopeArgs), ctypes.c_void_p]
         lib.dta_cast_f32.argtypes = [ctypes.c_int32] * 6 + [ctypes.c_void_p, DtaTensor, ctypes.c_void_p]
+        lib.dta_attn_decode.argtypes = [P(DecodeArgs), ctypes.c_void_p]
+        lib.dta_attn_decode_workspace_bytes.argtypes = [ctypes.c_int32] * 4
+        lib.dta_attn_decode_workspace_bytes.restype = ctypes.c_size_t
         lib.dta_attn_bwd_workspace_bytes.argtypes = [ctypes.c_int32] * 5
         lib.dta_attn_bwd_workspace_bytes.restype = ctypes.c_size_t
         lib.dta_error_string.argtypes = [ctypes.c_int]
         lib.dta_error_string.restype = ctypes.c_char_p
         lib.dta_supported.argtypes = [ctypes.c_int32] * 4
-        for fn in ("dta_attn_fwd", "dta_attn_bwd", "dta_ln_fwd", "dta_ln_bwd", "dta_rope", "dta_cast_f32",
+        for fn in ("dta_attn_fwd", "dta_attn_bwd", "dta_attn_decode", "dta_ln_fwd", "dta_ln_bwd", "dta_rope", "dta_cast_f32",
                    "dta_abi_version", "dta_supported"):
             getattr(lib, fn).restype = ctypes.c_int
         if lib.dta_abi_version() != ABI_VERSION:

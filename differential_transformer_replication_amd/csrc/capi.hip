@@ -226,4 +226,24 @@ int dta_cast_f32(int32_t dtype, int32_t B, int32_t T, int32_t H, int32_t n_terms
   return status(launch_cast(dtype, src, t5(dst), B, T, H, n_terms, head_size, (hipStream_t)stream));
 }
 
+size_t dta_attn_decode_workspace_bytes(int32_t B, int32_t H, int32_t n_terms, int32_t t_cap) {
+  return (size_t)B * H * n_terms * t_cap * 4;
+}
+
+int dta_attn_decode(const dta_attn_decode_args* a, void* stream) {
+  if (!a || !ok_dims(a->dtype, a->B, 1, a->H, a->n_terms, a->head_size, a->dv)) return DTA_ERR_INVALID;
+  if (a->head_size % 8 || a->head_size > 128 || a->n_terms > 4 || a->dv > 256) return DTA_ERR_UNSUPPORTED;
+  if (a->length < 1 || a->t_cap < a->length) return DTA_ERR_INVALID;
+  if ((int64_t)a->B * a->H == 0) return DTA_OK;
+  if (!ok_tensor(a->q, a->dtype, true) || !ok_tensor(a->k_cache, a->dtype, true) ||
+      !a->v_cache.ptr || !a->o.ptr || !a->coef || !aligned_ptr(a->workspace))
+    return DTA_ERR_INVALID;
+  DecodeParams p{};
+  p.q = t5(a->q); p.k = t5(a->k_cache); p.v = t5(a->v_cache); p.o = t5(a->o);
+  p.coef = a->coef; p.ws = a->workspace;
+  p.B = a->B; p.H = a->H; p.N = a->n_terms; p.HS = a->head_size; p.DV = a->dv;
+  p.L = a->length; p.ldw = a->t_cap; p.scale = a->scale;
+  return status(launch_decode(a->dtype, p, (hipStream_t)stream));
+}
+
 }  // extern "C"

@@ -63,6 +63,15 @@ struct DeltaParams {
   int B, T, H, N, DV;
 };
 
+struct DecodeParams {
+  T5 q, k, v, o;       // q/o: one row per (b, h) (st unused); k/v: the cache [b][t][h][i]
+  const float* coef;   // [h][i]
+  float* ws;           // fp32 [b][h][i][ldw]
+  int B, H, N, HS, DV, L, ldw;
+  float scale;
+};
+
+int launch_decode(int dtype, const DecodeParams& p, hipStream_t st);
 int launch_ln(int dtype, const LnParams& p, bool bwd, hipStream_t st);
 int launch_rope(int dtype, bool src_f32, const RopeParams& p, hipStream_t st);
 int launch_delta(int dtype, const DeltaParams& p, hipStream_t st);

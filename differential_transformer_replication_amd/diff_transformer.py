@@ -15,7 +15,7 @@ import torch
 import torch.nn as nn
 from torch.nn import functional as F
 
-from . import ops
+from . import kv_cache, ops
 from ._compat import (emit_tril_hooks, lambda_init_value, check_seq_len, check_dropout, fill_if_changed,
                       mha_out_scale)
 
@@ -196,6 +196,8 @@ class DiffTransformer(nn.Module):
     @torch.no_grad()
     def generate(self, idx, max_new_tokens):
         """Naive sampling: full forward per token, cropped to block_size (:177-185)."""
+        if kv_cache.enabled(idx):                        # KV-cache decode (SURVEY 8f item 4)
+            return kv_cache.cached_generate(self, idx, max_new_tokens)
         for _ in range(max_new_tokens):
             logits, _ = self(idx[:, -self.block_size:])
             probs = F.softmax(logits[:, -1, :], dim=-1)

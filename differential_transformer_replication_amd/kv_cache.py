@@ -1,0 +1,136 @@
+"""Incremental decoding for ``generate``.
+
+The reference's ``generate`` (diff_transformer.py:177-185; the same loop in
+Ndiff_transformer.py) runs a full forward over ``idx[:, -block_size:]`` for every
+new token and keeps only the last row of logits.  Here the first call runs the
+prompt once through the fused training kernels (prefill) and keeps every
+layer's K_i / V rows in a KV cache; each further token costs one projection row
+per layer and one ``dta_attn_decode`` launch (``ops.diff_attention_decode``)
+instead of a T x T recompute.
+
+Positions are absolute within the window (learned position table in
+DiffTransformer, RoPE rows in AlternatingDiffTransformer), so once the sequence
+outgrows ``block_size`` the window slides, every cached row changes position,
+and the step falls back to the reference's own full recompute of the cropped
+window.  Sampling (softmax of the last logits, ``torch.multinomial``) is the
+reference's, so with the same generator state the tokens match the
+full-recompute path whenever the logits agree to sampling precision.
+``DTA_KV_CACHE=0`` selects the full-recompute loop.
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict
+
+import torch
+from torch.nn import functional as F
+
+from . import ops
+from ._compat import mha_out_scale
+
+__all__ = ["KVCache", "cached_generate", "enabled"]
+
+
+def enabled(idx: torch.Tensor) -> bool:
+    return idx.is_cuda and os.environ.get("DTA_KV_CACHE", "1") != "0"
+
+
+class KVCache:
+    """Per-layer packed rows ``[K (H, N, hs) | V (H, dv)]`` of every cached position:
+    (B, block_size, H*N*hs + H*dv) in the projection's dtype, allocated once."""
+
+    def __init__(self):
+        self.rows: Dict[int, torch.Tensor] = {}
+        self.length = 0
+
+    def layer(self, layer: int, B: int, cap: int, width: int, like: torch.Tensor) -> torch.Tensor:
+        buf = self.rows.get(layer)
+        if buf is None or buf.shape != (B, cap, width) or buf.dtype != like.dtype:
+            buf = torch.empty(B, cap, width, device=like.device, dtype=like.dtype)
+            self.rows[layer] = buf
+        return buf
+
+
+def _attention_step(attn, x: torch.Tensor, layer: int, cache: KVCache, pos: int) -> torch.Tensor:
+    """MultiHead(Alternating)DiffAttention.forward for the rows at positions
+    pos .. pos+Tn-1, reading and extending the layer's cache."""
+    H, hs = attn.num_heads, attn.head_size
+    N = getattr(attn, "n_terms", 2)
+    dv = 2 * hs
+    rope = hasattr(attn.heads[0], "freqs_cis")
+    coef = attn.coefficients(layer)
+    qkv = F.linear(x, attn.packed_weight())
+    B, Tn, W = qkv.shape
+    nq = H * N * hs
+    buf = cache.layer(layer, B, attn.block_size, W - nq, qkv)
+    k_rows = buf[..., :nq].unflatten(-1, (H, N, hs))
+    freqs = None
+    if rope:
+        from .Ndiff_transformer import rope_table
+        freqs = rope_table(attn.heads[0].freqs_cis, pos + Tn, hs).to(device=x.device, dtype=torch.float32)
+    if pos == 0:
+        # prefill: the prompt through the training kernels, then cache its K_i / V rows
+        out = ops.diff_attention(qkv, coef, H, N, hs, freqs)
+        src = qkv[..., nq:2 * nq].unflatten(-1, (H, N, hs))
+        if rope:
+            ops.rope_rows(src, k_rows[:, :Tn], freqs[:Tn])
+        else:
+            k_rows[:, :Tn].copy_(src)
+        buf[:, :Tn, nq:].copy_(qkv[..., 2 * nq:])
+    else:
+        if Tn != 1:
+            raise RuntimeError("decode steps take one new position at a time")
+        q = qkv[:, :, :nq].unflatten(-1, (H, N, hs))               # (B, 1, H, N, hs)
+        src = qkv[:, :, nq:2 * nq].unflatten(-1, (H, N, hs))
+        if rope:
+            q_rot = torch.empty_like(q)
+            ops.rope_rows(q, q_rot, freqs[pos:pos + 1])
+            ops.rope_rows(src, k_rows[:, pos:pos + 1], freqs[pos:pos + 1])
+            q = q_rot
+        else:
+            k_rows[:, pos:pos + 1].copy_(src)
+        buf[:, pos, nq:].copy_(qkv[:, 0, 2 * nq:])
+        v_rows = buf[..., nq:].unflatten(-1, (H, dv))
+        out = ops.diff_attention_decode(q[:, 0], k_rows, v_rows, coef, pos + 1).view(B, 1, H * dv)
+    gn = attn.group_norm
+    out = ops.group_ln_scale(out, gn.weight, gn.bias, gn.eps, mha_out_scale(attn.lambda_init))
+    return attn.dropout(attn.proj(out))
+
+
+def _model_step(model, idx: torch.Tensor, cache: KVCache, pos: int) -> torch.Tensor:
+    """The model's forward (diff_transformer.py:154-175 / Ndiff_transformer.py) over
+    positions pos .. pos+T-1 of the window; returns the last row of logits."""
+    T = idx.shape[1]
+    x = model.token_embedding_table(idx)
+    if hasattr(model, "position_embedding_table"):
+        x = x + model.position_embedding_table(torch.arange(pos, pos + T, device=idx.device))
+    for layer, block in enumerate(model.blocks, 1):
+        x = x + _attention_step(block.diff_attn, block.ln1(x), layer, cache, pos)
+        x = x + block.ffwd(block.ln2(x))
+    return model.lm_head(model.ln_f(x[:, -1:]))[:, -1]
+
+
+def last_logits(model, idx: torch.Tensor, cache: KVCache) -> torch.Tensor:
+    """Logits of the newest position of ``idx``, reusing ``cache`` when the window
+    has not slid (exposed for the parity tests)."""
+    bs = model.block_size
+    if cache.length == 0 or idx.shape[1] > bs or idx.shape[1] != cache.length + 1:
+        cond = idx[:, -bs:]
+        cache.length = 0
+        logits = _model_step(model, cond, cache, 0)
+        cache.length = cond.shape[1] if idx.shape[1] < bs else 0    # a full window slides next step
+        return logits
+    logits = _model_step(model, idx[:, -1:], cache, cache.length)
+    cache.length += 1
+    if cache.length >= bs:
+        cache.length = 0
+    return logits
+
+
+@torch.no_grad()
+def cached_generate(model, idx: torch.Tensor, max_new_tokens: int) -> torch.Tensor:
+    cache = KVCache()
+    for _ in range(max_new_tokens):
+        probs = F.softmax(last_logits(model, idx, cache), dim=-1)
+        idx = torch.cat((idx, torch.multinomial(probs, num_samples=1)), dim=1)
+    return idx

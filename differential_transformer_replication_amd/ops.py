@@ -229,3 +229,45 @@ class _GroupLNScale(torch.autograd.Function):
 
 def group_ln_scale(x: Tensor, w: Tensor, b: Tensor, eps: float = 1e-5, out_scale: float = 1.0) -> Tensor:
     return _GroupLNScale.apply(x, w, b, eps, out_scale)
+
+
+# ------------------------------------------------------------------ decode ---
+def rope_rows(src: Tensor, dst: Tensor, table: Tensor) -> None:
+    """dst = RoPE(src) for (B, T, H, N, hs) views whose rows are the positions of
+    ``table`` (fp32 (T, hs/2, 2), already sliced to those positions).  No autograd:
+    the KV-cache path of generate() only (Ndiff_transformer.py:11-22, 104-109)."""
+    lib = _lib.load()
+    _require_gpu(src, dst, table)
+    B, T, H, N, hs = src.shape
+    table = table.to(device=src.device, dtype=torch.float32).contiguous()
+    ra = _lib.RopeArgs(_lib.dtype_code(dst.dtype), B, T, H, N, hs, 0, 0, _lib.tensor5(src), _lib.tensor5(dst),
+                       table.data_ptr())
+    _lib.check(lib.dta_rope(ra, _lib.stream_handle(src.device)))
+
+
+def diff_attention_decode(q: Tensor, k_cache: Tensor, v_cache: Tensor, coef: Tensor, length: int) -> Tensor:
+    """One new query row per (b, h) against the first ``length`` cached keys:
+    o = sum_i coef[h,i] softmax(q_i K_i[:length]^T / sqrt(hs)) V[:length].
+
+    q: (B, H, N, hs); k_cache: (B, T_cap, H, N, hs); v_cache: (B, T_cap, H, dv)
+    (strided views, innermost dim contiguous).  Returns (B, H*dv).  Equals the last
+    row of ``diff_attention`` over the same ``length`` positions (the causal mask
+    keeps every key up to the query's own position)."""
+    lib = _lib.load()
+    _require_gpu(q, k_cache, v_cache, coef)
+    B, H, N, hs = q.shape
+    T_cap, dv = k_cache.shape[1], v_cache.shape[-1]
+    if tuple(k_cache.shape) != (B, T_cap, H, N, hs) or tuple(v_cache.shape) != (B, T_cap, H, dv):
+        raise RuntimeError("k_cache/v_cache shapes do not match q")
+    if not 1 <= length <= T_cap:
+        raise RuntimeError(f"decode length {length} outside [1, {T_cap}]")
+    if q.dtype != k_cache.dtype or q.dtype != v_cache.dtype:
+        raise RuntimeError("q, k_cache and v_cache must share a dtype")
+    coef = coef.detach().to(torch.float32).contiguous()
+    o = torch.empty(B, 1, H, dv, device=q.device, dtype=q.dtype)
+    ws = torch.empty(B, H, N, T_cap, device=q.device, dtype=torch.float32)
+    a = _lib.DecodeArgs(_lib.dtype_code(q.dtype), B, H, N, hs, dv, length, T_cap, 1.0 / math.sqrt(hs),
+                        _lib.tensor5(q.unsqueeze(1)), _lib.tensor5(k_cache), _lib.tensor5(v_cache),
+                        _lib.tensor5(o), coef.data_ptr(), ws.data_ptr())
+    _lib.check(lib.dta_attn_decode(a, _lib.stream_handle(q.device)))
+    return o.view(B, H * dv)

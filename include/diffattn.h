@@ -153,6 +153,29 @@ typedef struct dta_rope_args {
 
 int dta_rope(const dta_rope_args* a, void* stream);
 
+/* One-token decode over a KV cache (incremental generate).
+ * Replaces, for the newest position only, the full-prefix recompute that
+ * generate() does per token (diff_transformer.py:177-185; the same loop in
+ * Ndiff_transformer.py and control.py:163-171): for every (b, h)
+ *   o = sum_i coef[h][i] * softmax(q_i . K_i[0:length]^T * scale) V[0:length]
+ * which is the last row of dta_attn_fwd's output at T = length (the newest key
+ * is the query's own position, so the causal mask keeps every cached key).
+ * q: [b][.][h][i][d] (st ignored), k_cache [b][t][h][i][d], v_cache [b][t][h][e],
+ * o [b][.][h][e] (st ignored).  head_size % 8 == 0, head_size <= 128,
+ * n_terms <= 4, dv <= 256.  workspace: fp32 [b][h][i][t_cap]
+ * (dta_attn_decode_workspace_bytes). */
+typedef struct dta_attn_decode_args {
+  int32_t dtype;
+  int32_t B, H, n_terms, head_size, dv;
+  int32_t length;            /* valid cached keys, including the new token's */
+  int32_t t_cap;             /* workspace row length (>= length) */
+  float scale;
+  dta_tensor q, k_cache, v_cache, o;
+  const float* coef;         /* fp32 [h][i] */
+  float* workspace;
+} dta_attn_decode_args;
+int dta_attn_decode(const dta_attn_decode_args* a, void* stream);
+size_t dta_attn_decode_workspace_bytes(int32_t B, int32_t H, int32_t n_terms, int32_t t_cap);
 /* Cast/copy a [b][t][h][i][d] tensor from fp32 to dtype (dQ finalisation). */
 int dta_cast_f32(int32_t dtype, int32_t B, int32_t T, int32_t H, int32_t n_terms,
                  int32_t head_size, const float* src, dta_tensor dst, void* stream);

@@ -1,0 +1,113 @@
+"""GPU parity of the KV-cache decode path.
+
+* ``dta_attn_decode`` against the oracle's ``diff_core`` (the reference's
+  combine-then-@V, diff_transformer.py:57-72 / Ndiff_transformer.py:102-125) in
+  fp64 on the CPU: the decode row must equal the LAST row of the full causal
+  attention over the same ``length`` positions.
+* The model-level incremental ``generate``: every step's last-row logits from the
+  cache path against a full forward of the same window (the reference's
+  generate loop, diff_transformer.py:177-185), through window slides past
+  block_size, for DiffTransformer (position table) and AlternatingDiffTransformer
+  (RoPE rows written into the cache); and equal sampled tokens for one seed.
+Tolerances (north_star): fp32 max|a-b|/max|b| <= 1e-4, bf16 <= 2e-2.
+"""
+import os
+
+import pytest
+import torch
+
+from conftest import rel_err
+from oracle import diffattn_oracle as O
+
+from differential_transformer_replication_amd import ops, kv_cache
+from differential_transformer_replication_amd import diff_transformer as D
+from differential_transformer_replication_amd import Ndiff_transformer as ND
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+TOL = {torch.float32: 1e-4, torch.bfloat16: 2e-2, torch.float16: 2e-2}
+
+
+def _decode_case(B, H, N, hs, dv, L, cap, dtype, seed):
+    g = torch.Generator().manual_seed(seed)
+    q = torch.randn(B, cap, H, N, hs, generator=g)
+    k = torch.randn(B, cap, H, N, hs, generator=g)
+    v = torch.randn(B, cap, H, dv, generator=g)
+    coef = torch.randn(H, N, generator=g) * 0.5
+    coef[:, 0] = 1.0
+    # oracle: full causal attention over positions 0..L-1, keep the last row
+    want = torch.empty(B, H, dv, dtype=torch.float64)
+    for h in range(H):
+        o = O.diff_core([q[:, :L, h, i].double() for i in range(N)], [k[:, :L, h, i].double() for i in range(N)],
+                        v[:, :L, h].double(), coef[h].double())
+        want[:, h] = o[:, -1]
+    qd, kd, vd = (t.to(DEV, dtype) for t in (q, k, v))
+    got = ops.diff_attention_decode(qd[:, L - 1], kd, vd, coef.to(DEV), L)
+    return got.view(B, H, dv), want
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("N,hs,dv", [(1, 64, 64), (2, 32, 64), (2, 64, 128), (3, 64, 128), (4, 32, 64),
+                                     (2, 128, 256), (1, 128, 128)])
+def test_decode_kernel_matches_oracle(dtype, N, hs, dv):
+    for L, cap in [(1, 1), (5, 9), (257, 300), (1000, 1024)]:
+        got, want = _decode_case(2, 3, N, hs, dv, L, cap, dtype, seed=L + 7 * N + hs)
+        assert rel_err(got.float(), want) <= TOL[dtype], (dtype, N, hs, dv, L)
+
+
+def test_decode_matches_fused_forward_last_row():
+    """Same inputs through dta_attn_fwd (T = L) and dta_attn_decode: last rows agree."""
+    B, H, N, hs, L = 2, 4, 2, 64, 384
+    dv = 2 * hs
+    g = torch.Generator().manual_seed(3)
+    qkv = torch.randn(B, L, ops.packed_width(H, N, hs, dv), generator=g).to(DEV)
+    coef = torch.tensor([[1.0, -0.6]] * H, device=DEV)
+    full = ops.diff_attention(qkv, coef, H, N, hs)[:, -1]
+    q, k, v = ops.split_packed(qkv, H, N, hs, dv)
+    dec = ops.diff_attention_decode(q[:, -1], k, v, coef, L)
+    assert rel_err(dec, full) <= 1e-4
+
+
+def test_decode_rejects_bad_length():
+    q = torch.zeros(1, 1, 2, 64, device=DEV)
+    k = torch.zeros(1, 8, 1, 2, 64, device=DEV)
+    v = torch.zeros(1, 8, 1, 128, device=DEV)
+    with pytest.raises(RuntimeError):
+        ops.diff_attention_decode(q, k, v, torch.ones(1, 2, device=DEV), 9)
+
+
+def _models():
+    torch.manual_seed(0)
+    yield "diff", D.DiffTransformer(vocab_size=97, n_embd=256, n_head=2, n_layer=2, block_size=24, dropout=0.0)
+    torch.manual_seed(1)
+    yield "alt3", ND.AlternatingDiffTransformer(97, 256, 2, 2, 24, 0.0, n_terms=3)
+
+
+@pytest.mark.parametrize("which", ["diff", "alt3"])
+def test_incremental_logits_match_full_forward(which):
+    model = dict(_models())[which].to(DEV).eval()
+    for p in model.parameters():          # non-zero lambdas so every branch weight differs
+        if p.dim() == 1 and p.shape[0] == 64:
+            torch.nn.init.normal_(p, std=0.1)
+    g = torch.Generator().manual_seed(5)
+    idx = torch.randint(0, 97, (2, 7), generator=g).to(DEV)
+    cache = kv_cache.KVCache()
+    with torch.no_grad():
+        for step in range(30):                           # crosses block_size 24: window slides
+            got = kv_cache.last_logits(model, idx, cache)
+            want = model(idx[:, -model.block_size:])[0][:, -1]
+            assert rel_err(got, want) <= 1e-4, (which, step, idx.shape[1])
+            idx = torch.cat([idx, torch.randint(0, 97, (2, 1), generator=g).to(DEV)], dim=1)
+
+
+@pytest.mark.parametrize("which", ["diff", "alt3"])
+def test_generate_tokens_match_full_recompute(which, monkeypatch):
+    model = dict(_models())[which].to(DEV).eval()
+    idx = torch.randint(0, 97, (2, 5), generator=torch.Generator().manual_seed(9)).to(DEV)
+    torch.manual_seed(1234)
+    fast = model.generate(idx, 30)
+    monkeypatch.setenv("DTA_KV_CACHE", "0")
+    torch.manual_seed(1234)
+    slow = model.generate(idx, 30)
+    assert fast.shape == (2, 35)
+    assert torch.equal(fast, slow)
