@@ -254,12 +254,49 @@ def kernel_bench(args, world, rank):
     return res
 
 
+def decode_bench(args, world, rank):
+    """--mode decode: one KV-cache decode launch (dta_attn_decode) per step, bf16,
+    cache length L = --seq.  HBM-bound: algorithmic bytes per launch =
+    B*H*L*(N*hs + dv)*2 (every cached K_i / V row read once)."""
+    from differential_transformer_replication_amd import ops
+    B, H, hs, N, L = args.batch, args.heads, args.head_size, args.n_terms, args.seq
+    dv = 2 * hs
+    dev = torch.device("cuda", torch.cuda.current_device())
+    g = torch.Generator(device=dev).manual_seed(0)
+    k = torch.randn(B, L, H, N, hs, device=dev, dtype=torch.bfloat16, generator=g)
+    v = torch.randn(B, L, H, dv, device=dev, dtype=torch.bfloat16, generator=g)
+    q = torch.randn(B, H, N, hs, device=dev, dtype=torch.bfloat16, generator=g)
+    coef = torch.tensor([[1.0, -0.5, 0.3, -0.2][:N]] * H, device=dev)
+    for _ in range(args.warmup):
+        ops.diff_attention_decode(q, k, v, coef, L)
+    _sync(world)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for e0, e1 in ev:
+        e0.record()
+        ops.diff_attention_decode(q, k, v, coef, L)
+        e1.record()
+    _sync(world)
+    ms = _max_over_ranks((time.perf_counter() - t0) * 1e3 / args.steps, world)
+    kms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
+    nbytes = B * H * L * (N * hs + dv) * 2
+    return {"metric": "KV-cache decode attention GB/s (one new token per sequence)", "value": round(
+        world * nbytes / ms / 1e6, 1), "unit": "GB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(ms, 5), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "bf16", "data": "synthetic",
+        "config": {"workload": "decode: one query row per (b, h) over an L-row KV cache", "batch_per_gpu": B,
+                   "heads": H, "head_size": hs, "dv": dv, "n_terms": N, "cache_len": L},
+        "roofline": {"bound": "hbm", "kernel": "decode_kernel", "achieved": round(nbytes / kms / 1e6, 1),
+                     "peak": 8000.0, "unit": "GB/s", "frac": round(nbytes / kms / 1e6 / 8000.0, 4),
+                     "traffic": None, "kernel_ms": round(kms, 5), "alg_bytes": nbytes}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--mode", choices=["kernel", "train"], default="kernel")
+    ap.add_argument("--mode", choices=["kernel", "train", "decode"], default="kernel")
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--seq", type=int, default=4096)
     ap.add_argument("--heads", type=int, default=16)
@@ -276,6 +313,8 @@ def main():
     world, rank, local = _dist()
     if args.mode == "kernel":
         res = kernel_bench(args, world, rank)
+    elif args.mode == "decode":
+        res = decode_bench(args, world, rank)
     else:
         from differential_transformer_replication_amd.train import train_bench
         res = train_bench(args, world, rank)

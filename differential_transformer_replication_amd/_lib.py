@@ -103,7 +103,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         lib.dta_rope.argtypes = [P(RopeArgs), ctypes.c_void_p]
         lib.dta_cast_f32.argtypes = [ctypes.c_int32] * 6 + [ctypes.c_void_p, DtaTensor, ctypes.c_void_p]
         lib.dta_attn_decode.argtypes = [P(DecodeArgs), ctypes.c_void_p]
-        lib.dta_attn_decode_workspace_bytes.argtypes = [ctypes.c_int32] * 4
+        lib.dta_attn_decode_workspace_bytes.argtypes = [ctypes.c_int32] * 6
         lib.dta_attn_decode_workspace_bytes.restype = ctypes.c_size_t
         lib.dta_attn_bwd_workspace_bytes.argtypes = [ctypes.c_int32] * 5
         lib.dta_attn_bwd_workspace_bytes.restype = ctypes.c_size_t

@@ -226,8 +226,13 @@ int dta_cast_f32(int32_t dtype, int32_t B, int32_t T, int32_t H, int32_t n_terms
   return status(launch_cast(dtype, src, t5(dst), B, T, H, n_terms, head_size, (hipStream_t)stream));
 }
 
-size_t dta_attn_decode_workspace_bytes(int32_t B, int32_t H, int32_t n_terms, int32_t t_cap) {
-  return (size_t)B * H * n_terms * t_cap * 4;
+static int64_t decode_splits(int32_t t_cap) { return (t_cap + 255) / 256; }
+
+size_t dta_attn_decode_workspace_bytes(int32_t B, int32_t H, int32_t n_terms, int32_t head_size, int32_t dv,
+                                       int32_t t_cap) {
+  const size_t single = (size_t)B * H * n_terms * t_cap * 4;
+  const size_t split = (size_t)B * H * decode_splits(t_cap) * n_terms * (dv + 2) * 4;
+  return single > split ? single : split;
 }
 
 int dta_attn_decode(const dta_attn_decode_args* a, void* stream) {
@@ -243,6 +248,8 @@ int dta_attn_decode(const dta_attn_decode_args* a, void* stream) {
   p.coef = a->coef; p.ws = a->workspace;
   p.B = a->B; p.H = a->H; p.N = a->n_terms; p.HS = a->head_size; p.DV = a->dv;
   p.L = a->length; p.ldw = a->t_cap; p.scale = a->scale;
+  p.S = (int)decode_splits(a->length);
+  p.ml = a->workspace + (int64_t)a->B * a->H * p.S * a->n_terms * a->dv;   // after the partial rows
   return status(launch_decode(a->dtype, p, (hipStream_t)stream));
 }
 

@@ -12,6 +12,7 @@
 //   phase 3  w_j = sum_i coef_i e_ij / l_i (the combined map row)
 //   phase 4  o[e] = sum_j w_j V[j][e]: threads own a column, key groups stride
 //            (coalesced V rows), LDS reduction over the groups.
+// The split-key plan below is the one used for the standard head sizes.
 // Algorithmic bytes per (b, h) and token: L * (N*hs + dv) * sizeof(E).
 #include "dta_common.h"
 #include "dta_internal.h"
@@ -143,8 +144,165 @@ __global__ __launch_bounds__(kThreads) void decode_kernel(DecodeParams p) {
   }
 }
 
+// ---- split-key path (flash-decoding): fills the chip when B*H is small ------
+// Grid (S, H, B): workgroup s owns keys [s*kChunk, (s+1)*kChunk).  It writes,
+// per branch i, the chunk's max m_i, sum l_i = sum_j exp(s_ij - m_i) and the
+// un-normalised row acc_i = sum_j exp(s_ij - m_i) V_j (fp32).  decode_combine
+// rescales the S partials to the global max and applies coef_i / L_i.
+// K rows are read by LPR = HS/8 lanes each (one 16-byte load per lane), V rows
+// by DV/8 lanes each, so every wave-level load is a run of whole rows.
+constexpr int kChunk = 256;
+
+template <class E, int N, int HS, int DV>
+__global__ __launch_bounds__(kThreads) void decode_split_kernel(DecodeParams p) {
+  constexpr int LPR = HS / 8;                 // lanes per K row
+  constexpr int KPW = 64 / LPR;               // keys per wave per load
+  constexpr int VPR = DV / 8;                 // lanes per V row
+  constexpr int G = kThreads / VPR;           // V row groups
+  __shared__ float sc[N][kChunk];
+  __shared__ float red[kWaves * N];
+  __shared__ float part[G][N][DV + 4];
+  const int s = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int j0 = s * kChunk, L = p.L;
+  const int nk = min(kChunk, L - j0);
+
+  // phase 1: scores of this chunk into LDS
+  {
+    const int sub = lane % LPR, kr = lane / LPR;
+    const E* gq = reinterpret_cast<const E*>(p.q.p) + b * p.q.sb + h * p.q.sh + sub * 8;
+    float q[N][8];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      ld8f<E>(gq + i * p.q.si, q[i]);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) q[i][u] *= p.scale;
+    }
+    const E* gk = reinterpret_cast<const E*>(p.k.p) + b * p.k.sb + h * p.k.sh + sub * 8;
+    for (int jj = wave * KPW + kr; jj < kChunk; jj += kWaves * KPW) {
+      const bool ok = jj < nk;
+      const E* kp = gk + (int64_t)(j0 + (ok ? jj : 0)) * p.k.st;
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        float f[8];
+        ld8f<E>(kp + i * p.k.si, f);
+        float d = 0.f;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) d = fmaf(q[i][u], f[u], d);
+#pragma unroll
+        for (int o = LPR / 2; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
+        if (sub == 0) sc[i][jj] = ok ? d : -INFINITY;
+      }
+    }
+  }
+  __syncthreads();
+
+  // phase 2: chunk max / exp / sum per branch (thread = key)
+  float m[N], l[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) m[i] = sc[i][tid];
+  block_reduce<N, true>(m, red);
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const float e = tid < nk ? __expf(sc[i][tid] - m[i]) : 0.f;
+    sc[i][tid] = e;
+    l[i] = e;
+  }
+  block_reduce<N, false>(l, red);        // its barriers also publish sc
+
+  // phase 3: acc_i = sum_j e_ij V_j (thread = 8 columns of one row group)
+  const int g = tid / VPR, c0 = (tid % VPR) * 8;
+  const E* gv = reinterpret_cast<const E*>(p.v.p) + b * p.v.sb + h * p.v.sh + c0;
+  float acc[N][8];
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc[i][u] = 0.f;
+  for (int jj = g; jj < nk; jj += G) {
+    float f[8];
+    ld8f<E>(gv + (int64_t)(j0 + jj) * p.v.st, f);
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const float e = sc[i][jj];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc[i][u] = fmaf(e, f[u], acc[i][u]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+#pragma unroll
+    for (int u = 0; u < 8; ++u) part[g][i][c0 + u] = acc[i][u];
+  __syncthreads();
+  const int64_t row = ((int64_t)b * p.H + h) * p.S + s;      // partial index
+  float* wacc = p.ws + row * N * DV;
+  for (int x = tid; x < N * DV; x += kThreads) {
+    const int i = x / DV, c = x % DV;
+    float a = 0.f;
+#pragma unroll
+    for (int gg = 0; gg < G; ++gg) a += part[gg][i][c];
+    wacc[x] = a;
+  }
+  if (tid < N) {
+    p.ml[row * N * 2 + tid * 2] = m[tid];
+    p.ml[row * N * 2 + tid * 2 + 1] = l[tid];
+  }
+}
+
+template <class E, int N>
+__global__ __launch_bounds__(kThreads) void decode_combine_kernel(DecodeParams p) {
+  const int h = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const int64_t row0 = ((int64_t)b * p.H + h) * p.S;
+  const float* ml = p.ml + row0 * N * 2;
+  float M[N], Ls[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    M[i] = -INFINITY;
+    for (int s = 0; s < p.S; ++s) M[i] = fmaxf(M[i], ml[s * N * 2 + i * 2]);
+    Ls[i] = 0.f;
+    for (int s = 0; s < p.S; ++s) Ls[i] += ml[s * N * 2 + i * 2 + 1] * __expf(ml[s * N * 2 + i * 2] - M[i]);
+    Ls[i] = p.coef[h * N + i] / Ls[i];
+  }
+  E* go = reinterpret_cast<E*>(p.o.p) + b * p.o.sb + h * p.o.sh;
+  for (int c = tid; c < p.DV; c += kThreads) {
+    float o = 0.f;
+    for (int s = 0; s < p.S; ++s) {
+      const float* a = p.ws + (row0 + s) * N * p.DV;
+#pragma unroll
+      for (int i = 0; i < N; ++i) o = fmaf(Ls[i] * __expf(ml[s * N * 2 + i * 2] - M[i]), a[i * p.DV + c], o);
+    }
+    go[c] = (E)o;
+  }
+}
+
+template <class E, int N, int HS, int DV>
+int split_launch(const DecodeParams& p, hipStream_t st) {
+  hipLaunchKernelGGL((decode_split_kernel<E, N, HS, DV>), dim3(p.S, p.H, p.B), dim3(kThreads), 0, st, p);
+  hipLaunchKernelGGL((decode_combine_kernel<E, N>), dim3(p.H, p.B), dim3(kThreads), 0, st, p);
+  return (int)hipGetLastError();
+}
+
+template <class E, int N>
+int split_dispatch(const DecodeParams& p, hipStream_t st) {
+  if (p.HS == 32 && p.DV == 64) return split_launch<E, N, 32, 64>(p, st);
+  if (p.HS == 64 && p.DV == 128) return split_launch<E, N, 64, 128>(p, st);
+  if (p.HS == 128 && p.DV == 256) return split_launch<E, N, 128, 256>(p, st);
+  if (N == 1 && p.HS == 64 && p.DV == 64) return split_launch<E, N, 64, 64>(p, st);
+  if (N == 1 && p.HS == 128 && p.DV == 128) return split_launch<E, N, 128, 128>(p, st);
+  return 1;    // no split plan: caller uses the single-pass kernel
+}
+
 template <class E>
 int decode_launch(const DecodeParams& p, hipStream_t st) {
+  if (p.ml) {
+    int e = 1;
+    switch (p.N) {
+      case 1: e = split_dispatch<E, 1>(p, st); break;
+      case 2: e = split_dispatch<E, 2>(p, st); break;
+      case 3: e = split_dispatch<E, 3>(p, st); break;
+      case 4: e = split_dispatch<E, 4>(p, st); break;
+    }
+    if (e != 1) return e;
+  }
   dim3 g(p.H, p.B);
   switch (p.N) {
     case 1: hipLaunchKernelGGL((decode_kernel<E, 1>), g, dim3(kThreads), 0, st, p); break;

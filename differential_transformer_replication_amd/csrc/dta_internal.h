@@ -66,8 +66,9 @@ struct DeltaParams {
 struct DecodeParams {
   T5 q, k, v, o;       // q/o: one row per (b, h) (st unused); k/v: the cache [b][t][h][i]
   const float* coef;   // [h][i]
-  float* ws;           // fp32 [b][h][i][ldw]
-  int B, H, N, HS, DV, L, ldw;
+  float* ws;           // single pass: fp32 [b][h][i][ldw]; split: partial rows [b][h][s][i][DV]
+  float* ml;           // split path: fp32 [b][h][s][i][2] chunk (max, sum); null = single pass
+  int B, H, N, HS, DV, L, ldw, S;
   float scale;
 };
 

@@ -265,7 +265,8 @@ def diff_attention_decode(q: Tensor, k_cache: Tensor, v_cache: Tensor, coef: Ten
         raise RuntimeError("q, k_cache and v_cache must share a dtype")
     coef = coef.detach().to(torch.float32).contiguous()
     o = torch.empty(B, 1, H, dv, device=q.device, dtype=q.dtype)
-    ws = torch.empty(B, H, N, T_cap, device=q.device, dtype=torch.float32)
+    nbytes = lib.dta_attn_decode_workspace_bytes(B, H, N, hs, dv, T_cap)
+    ws = torch.empty(nbytes // 4, device=q.device, dtype=torch.float32)
     a = _lib.DecodeArgs(_lib.dtype_code(q.dtype), B, H, N, hs, dv, length, T_cap, 1.0 / math.sqrt(hs),
                         _lib.tensor5(q.unsqueeze(1)), _lib.tensor5(k_cache), _lib.tensor5(v_cache),
                         _lib.tensor5(o), coef.data_ptr(), ws.data_ptr())

@@ -162,8 +162,11 @@ int dta_rope(const dta_rope_args* a, void* stream);
  * is the query's own position, so the causal mask keeps every cached key).
  * q: [b][.][h][i][d] (st ignored), k_cache [b][t][h][i][d], v_cache [b][t][h][e],
  * o [b][.][h][e] (st ignored).  head_size % 8 == 0, head_size <= 128,
- * n_terms <= 4, dv <= 256.  workspace: fp32 [b][h][i][t_cap]
- * (dta_attn_decode_workspace_bytes). */
+ * n_terms <= 4, dv <= 256.  workspace: fp32, dta_attn_decode_workspace_bytes
+ * (covers both plans: a split-key plan -- 256-key chunks scored by separate
+ * workgroups, then one combine launch -- for (head_size, dv) in {(32,64),
+ * (64,128), (128,256)} and, with n_terms = 1, dv = head_size in {64, 128};
+ * a single-pass workgroup per (b, h) otherwise). */
 typedef struct dta_attn_decode_args {
   int32_t dtype;
   int32_t B, H, n_terms, head_size, dv;
@@ -175,7 +178,8 @@ typedef struct dta_attn_decode_args {
   float* workspace;
 } dta_attn_decode_args;
 int dta_attn_decode(const dta_attn_decode_args* a, void* stream);
-size_t dta_attn_decode_workspace_bytes(int32_t B, int32_t H, int32_t n_terms, int32_t t_cap);
+size_t dta_attn_decode_workspace_bytes(int32_t B, int32_t H, int32_t n_terms, int32_t head_size, int32_t dv,
+                                       int32_t t_cap);
 /* Cast/copy a [b][t][h][i][d] tensor from fp32 to dtype (dQ finalisation). */
 int dta_cast_f32(int32_t dtype, int32_t B, int32_t T, int32_t H, int32_t n_terms,
                  int32_t head_size, const float* src, dta_tensor dst, void* stream);
