@@ -248,29 +248,45 @@ __global__ __launch_bounds__(kThreads) void decode_split_kernel(DecodeParams p) 
   }
 }
 
+constexpr int kMaxPartials = 2048;            // S * N per (b, h) for the combine's LDS weights
+
 template <class E, int N>
 __global__ __launch_bounds__(kThreads) void decode_combine_kernel(DecodeParams p) {
+  __shared__ float wgt[kMaxPartials];          // [s][i] = coef_i / L_i * exp(m_is - M_i)
+  __shared__ float red[kWaves * N];
   const int h = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
-  const int64_t row0 = ((int64_t)b * p.H + h) * p.S;
+  const int S = p.S;
+  const int64_t row0 = ((int64_t)b * p.H + h) * S;
   const float* ml = p.ml + row0 * N * 2;
   float M[N], Ls[N];
 #pragma unroll
   for (int i = 0; i < N; ++i) {
     M[i] = -INFINITY;
-    for (int s = 0; s < p.S; ++s) M[i] = fmaxf(M[i], ml[s * N * 2 + i * 2]);
-    Ls[i] = 0.f;
-    for (int s = 0; s < p.S; ++s) Ls[i] += ml[s * N * 2 + i * 2 + 1] * __expf(ml[s * N * 2 + i * 2] - M[i]);
-    Ls[i] = p.coef[h * N + i] / Ls[i];
+    for (int s = tid; s < S; s += kThreads) M[i] = fmaxf(M[i], ml[s * N * 2 + i * 2]);
   }
-  E* go = reinterpret_cast<E*>(p.o.p) + b * p.o.sb + h * p.o.sh;
-  for (int c = tid; c < p.DV; c += kThreads) {
-    float o = 0.f;
-    for (int s = 0; s < p.S; ++s) {
-      const float* a = p.ws + (row0 + s) * N * p.DV;
+  block_reduce<N, true>(M, red);
 #pragma unroll
-      for (int i = 0; i < N; ++i) o = fmaf(Ls[i] * __expf(ml[s * N * 2 + i * 2] - M[i]), a[i * p.DV + c], o);
+  for (int i = 0; i < N; ++i) {
+    Ls[i] = 0.f;
+    for (int s = tid; s < S; s += kThreads) {
+      const float e = __expf(ml[s * N * 2 + i * 2] - M[i]);
+      wgt[s * N + i] = e;
+      Ls[i] += ml[s * N * 2 + i * 2 + 1] * e;
     }
-    go[c] = (E)o;
+  }
+  block_reduce<N, false>(Ls, red);             // barriers also publish wgt
+  E* go = reinterpret_cast<E*>(p.o.p) + b * p.o.sb + h * p.o.sh;
+  const float* a = p.ws + row0 * N * p.DV;
+  float c[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) c[i] = p.coef[h * N + i] / Ls[i];
+  for (int col = tid; col < p.DV; col += kThreads) {
+    float o = 0.f;
+#pragma unroll 4
+    for (int s = 0; s < S; ++s)
+#pragma unroll
+      for (int i = 0; i < N; ++i) o = fmaf(c[i] * wgt[s * N + i], a[((int64_t)s * N + i) * p.DV + col], o);
+    go[col] = (E)o;
   }
 }
 
@@ -293,7 +309,7 @@ int split_dispatch(const DecodeParams& p, hipStream_t st) {
 
 template <class E>
 int decode_launch(const DecodeParams& p, hipStream_t st) {
-  if (p.ml) {
+  if (p.ml && p.S * p.N <= kMaxPartials) {
     int e = 1;
     switch (p.N) {
       case 1: e = split_dispatch<E, 1>(p, st); break;
