@@ -42,6 +42,9 @@ class KVCache:
     def __init__(self):
         self.rows: Dict[int, torch.Tensor] = {}
         self.length = 0
+        # parameters do not change inside generate(): the packed projection weight,
+        # the branch coefficients and the RoPE table are built once per layer
+        self.consts: Dict[int, tuple] = {}
 
     def layer(self, layer: int, B: int, cap: int, width: int, like: torch.Tensor) -> torch.Tensor:
         buf = self.rows.get(layer)
@@ -57,20 +60,25 @@ def _attention_step(attn, x: torch.Tensor, layer: int, cache: KVCache, pos: int)
     H, hs = attn.num_heads, attn.head_size
     N = getattr(attn, "n_terms", 2)
     dv = 2 * hs
-    rope = hasattr(attn.heads[0], "freqs_cis")
-    coef = attn.coefficients(layer)
-    qkv = F.linear(x, attn.packed_weight())
+    consts = cache.consts.get(layer)
+    if consts is None:
+        freqs = None
+        if hasattr(attn.heads[0], "freqs_cis"):
+            from .Ndiff_transformer import rope_table
+            freqs = rope_table(attn.heads[0].freqs_cis, attn.block_size, hs).to(
+                device=x.device, dtype=torch.float32).contiguous()
+        consts = (attn.packed_weight(), attn.coefficients(layer), freqs)
+        cache.consts[layer] = consts
+    weight, coef, freqs = consts
+    rope = freqs is not None
+    qkv = F.linear(x, weight)
     B, Tn, W = qkv.shape
     nq = H * N * hs
     buf = cache.layer(layer, B, attn.block_size, W - nq, qkv)
     k_rows = buf[..., :nq].unflatten(-1, (H, N, hs))
-    freqs = None
-    if rope:
-        from .Ndiff_transformer import rope_table
-        freqs = rope_table(attn.heads[0].freqs_cis, pos + Tn, hs).to(device=x.device, dtype=torch.float32)
     if pos == 0:
         # prefill: the prompt through the training kernels, then cache its K_i / V rows
-        out = ops.diff_attention(qkv, coef, H, N, hs, freqs)
+        out = ops.diff_attention(qkv, coef, H, N, hs, None if freqs is None else freqs[:Tn])
         src = qkv[..., nq:2 * nq].unflatten(-1, (H, N, hs))
         if rope:
             ops.rope_rows(src, k_rows[:, :Tn], freqs[:Tn])
