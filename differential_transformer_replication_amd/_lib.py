@@ -78,7 +78,7 @@ class DecodeArgs(ctypes.Structure):
                 ("n_terms", ctypes.c_int32), ("head_size", ctypes.c_int32), ("dv", ctypes.c_int32),
                 ("length", ctypes.c_int32), ("t_cap", ctypes.c_int32), ("scale", ctypes.c_float),
                 ("q", DtaTensor), ("k_cache", DtaTensor), ("v_cache", DtaTensor), ("o", DtaTensor),
-                ("coef", ctypes.c_void_p), ("workspace", ctypes.c_void_p)]
+                ("coef", ctypes.c_void_p), ("workspace", ctypes.c_void_p), ("length_dev", ctypes.c_void_p)]
 
 
 _lock = threading.Lock()

@@ -247,7 +247,7 @@ int dta_attn_decode(const dta_attn_decode_args* a, void* stream) {
   p.q = t5(a->q); p.k = t5(a->k_cache); p.v = t5(a->v_cache); p.o = t5(a->o);
   p.coef = a->coef; p.ws = a->workspace;
   p.B = a->B; p.H = a->H; p.N = a->n_terms; p.HS = a->head_size; p.DV = a->dv;
-  p.L = a->length; p.ldw = a->t_cap; p.scale = a->scale;
+  p.L = a->length; p.ldw = a->t_cap; p.scale = a->scale; p.Ldev = a->length_dev;
   p.S = (int)decode_splits(a->length);
   p.ml = a->workspace + (int64_t)a->B * a->H * p.S * a->n_terms * a->dv;   // after the partial rows
   return status(launch_decode(a->dtype, p, (hipStream_t)stream));

@@ -75,7 +75,7 @@ __global__ __launch_bounds__(kThreads) void decode_kernel(DecodeParams p) {
   __shared__ float red[kWaves * N];
   __shared__ float part[kThreads];
   const int h = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
-  const int HS = p.HS, DV = p.DV, L = p.L;
+  const int HS = p.HS, DV = p.DV, L = p.Ldev ? *p.Ldev : p.L;
   const E* gq = reinterpret_cast<const E*>(p.q.p) + b * p.q.sb + h * p.q.sh;
   for (int x = tid; x < N * HS; x += kThreads) qs[x] = (float)gq[(x / HS) * p.q.si + x % HS];
   __syncthreads();
@@ -164,7 +164,8 @@ __global__ __launch_bounds__(kThreads) void decode_split_kernel(DecodeParams p) 
   __shared__ float part[G][N][DV + 4];
   const int s = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int j0 = s * kChunk, L = p.L;
+  const int j0 = s * kChunk, L = p.Ldev ? *p.Ldev : p.L;
+  if (j0 >= L) return;                         // grid sized for an upper bound (uniform exit)
   const int nk = min(kChunk, L - j0);
 
   // phase 1: scores of this chunk into LDS
@@ -255,8 +256,8 @@ __global__ __launch_bounds__(kThreads) void decode_combine_kernel(DecodeParams p
   __shared__ float wgt[kMaxPartials];          // [s][i] = coef_i / L_i * exp(m_is - M_i)
   __shared__ float red[kWaves * N];
   const int h = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
-  const int S = p.S;
-  const int64_t row0 = ((int64_t)b * p.H + h) * S;
+  const int64_t row0 = ((int64_t)b * p.H + h) * p.S;       // partial stride: the launch's S
+  const int S = p.Ldev ? (*p.Ldev + kChunk - 1) / kChunk : p.S;  // chunks written this call
   const float* ml = p.ml + row0 * N * 2;
   float M[N], Ls[N];
 #pragma unroll

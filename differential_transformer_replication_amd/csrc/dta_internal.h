@@ -68,8 +68,9 @@ struct DecodeParams {
   const float* coef;   // [h][i]
   float* ws;           // single pass: fp32 [b][h][i][ldw]; split: partial rows [b][h][s][i][DV]
   float* ml;           // split path: fp32 [b][h][s][i][2] chunk (max, sum); null = single pass
-  int B, H, N, HS, DV, L, ldw, S;
+  int B, H, N, HS, DV, L, ldw, S;   // L: length, or its upper bound when Ldev is set
   float scale;
+  const int* Ldev;     // optional device length
 };
 
 int launch_decode(int dtype, const DecodeParams& p, hipStream_t st);

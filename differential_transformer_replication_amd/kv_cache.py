@@ -15,7 +15,10 @@ and the step falls back to the reference's own full recompute of the cropped
 window.  Sampling (softmax of the last logits, ``torch.multinomial``) is the
 reference's, so with the same generator state the tokens match the
 full-recompute path whenever the logits agree to sampling precision.
-``DTA_KV_CACHE=0`` selects the full-recompute loop.
+``DTA_KV_CACHE=0`` selects the full-recompute loop.  Decode steps replay one
+captured HIP graph of the whole model step (the position lives on the device,
+``dta_attn_decode`` reads its length there); ``DTA_DECODE_GRAPH=0`` launches
+them eagerly instead.
 """
 from __future__ import annotations
 
@@ -28,7 +31,7 @@ from torch.nn import functional as F
 from . import ops
 from ._compat import mha_out_scale
 
-__all__ = ["KVCache", "cached_generate", "enabled"]
+__all__ = ["KVCache", "DecodeGraph", "DevicePosition", "cached_generate", "enabled"]
 
 
 def enabled(idx: torch.Tensor) -> bool:
@@ -45,6 +48,8 @@ class KVCache:
         # parameters do not change inside generate(): the packed projection weight,
         # the branch coefficients and the RoPE table are built once per layer
         self.consts: Dict[int, tuple] = {}
+        self.graph = None
+        self.use_graph = os.environ.get("DTA_DECODE_GRAPH", "1") != "0"
 
     def layer(self, layer: int, B: int, cap: int, width: int, like: torch.Tensor) -> torch.Tensor:
         buf = self.rows.get(layer)
@@ -88,21 +93,68 @@ def _attention_step(attn, x: torch.Tensor, layer: int, cache: KVCache, pos: int)
     else:
         if Tn != 1:
             raise RuntimeError("decode steps take one new position at a time")
+        dev = isinstance(pos, DevicePosition)
         q = qkv[:, :, :nq].unflatten(-1, (H, N, hs))               # (B, 1, H, N, hs)
-        src = qkv[:, :, nq:2 * nq].unflatten(-1, (H, N, hs))
-        if rope:
-            q_rot = torch.empty_like(q)
-            ops.rope_rows(q, q_rot, freqs[pos:pos + 1])
-            ops.rope_rows(src, k_rows[:, pos:pos + 1], freqs[pos:pos + 1])
-            q = q_rot
-        else:
-            k_rows[:, pos:pos + 1].copy_(src)
-        buf[:, pos, nq:].copy_(qkv[:, 0, 2 * nq:])
+        k_new = qkv[:, :, nq:2 * nq].unflatten(-1, (H, N, hs))
+        v_new = qkv[:, :, 2 * nq:].unflatten(-1, (H, dv))
         v_rows = buf[..., nq:].unflatten(-1, (H, dv))
-        out = ops.diff_attention_decode(q[:, 0], k_rows, v_rows, coef, pos + 1).view(B, 1, H * dv)
+        if rope:
+            tab = freqs.index_select(0, pos.idx) if dev else freqs[pos:pos + 1]
+            q_rot, k_rot = torch.empty_like(q), torch.empty_like(k_new)
+            ops.rope_rows(q, q_rot, tab)
+            ops.rope_rows(k_new, k_rot, tab)
+            q, k_new = q_rot, k_rot
+        if dev:                                   # graph-replayable: position read on the device
+            k_rows.index_copy_(1, pos.idx, k_new)
+            v_rows.index_copy_(1, pos.idx, v_new)
+            out = ops.diff_attention_decode(q[:, 0], k_rows, v_rows, coef, attn.block_size, pos.length)
+        else:
+            k_rows[:, pos:pos + 1].copy_(k_new)
+            v_rows[:, pos:pos + 1].copy_(v_new)
+            out = ops.diff_attention_decode(q[:, 0], k_rows, v_rows, coef, pos + 1)
+        out = out.view(B, 1, H * dv)
     gn = attn.group_norm
     out = ops.group_ln_scale(out, gn.weight, gn.bias, gn.eps, mha_out_scale(attn.lambda_init))
     return attn.dropout(attn.proj(out))
+
+
+class DevicePosition:
+    """The decode position held on the device (index and index + 1), so one
+    captured graph replays for every position."""
+
+    def __init__(self, device):
+        self.idx = torch.zeros(1, dtype=torch.long, device=device)
+        self.length = torch.ones(1, dtype=torch.int32, device=device)
+
+    def set(self, p: int) -> None:
+        self.idx.fill_(p)
+        self.length.fill_(p + 1)
+
+
+class DecodeGraph:
+    """One decode step (every layer, Tn = 1) captured as a HIP graph: per token the
+    host issues two fills and one graph launch instead of ~15 launches per layer."""
+
+    def __init__(self, model, cache: "KVCache", B: int, device):
+        self.tok = torch.zeros(B, 1, dtype=torch.long, device=device)
+        self.pos = DevicePosition(device)
+        # warm-up (allocator, cached constants) writes cache row block_size-1 only,
+        # which is rewritten before it is ever read
+        self.pos.set(model.block_size - 1)
+        side = torch.cuda.Stream(device)
+        side.wait_stream(torch.cuda.current_stream(device))
+        with torch.cuda.stream(side):
+            _model_step(model, self.tok, cache, self.pos)
+        torch.cuda.current_stream(device).wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.logits = _model_step(model, self.tok, cache, self.pos)
+
+    def step(self, tok: torch.Tensor, p: int) -> torch.Tensor:
+        self.tok.copy_(tok)
+        self.pos.set(p)
+        self.graph.replay()
+        return self.logits.clone()
 
 
 def _model_step(model, idx: torch.Tensor, cache: KVCache, pos: int) -> torch.Tensor:
@@ -111,7 +163,8 @@ def _model_step(model, idx: torch.Tensor, cache: KVCache, pos: int) -> torch.Ten
     T = idx.shape[1]
     x = model.token_embedding_table(idx)
     if hasattr(model, "position_embedding_table"):
-        x = x + model.position_embedding_table(torch.arange(pos, pos + T, device=idx.device))
+        rows = pos.idx if isinstance(pos, DevicePosition) else torch.arange(pos, pos + T, device=idx.device)
+        x = x + model.position_embedding_table(rows)
     for layer, block in enumerate(model.blocks, 1):
         x = x + _attention_step(block.diff_attn, block.ln1(x), layer, cache, pos)
         x = x + block.ffwd(block.ln2(x))
@@ -128,7 +181,12 @@ def last_logits(model, idx: torch.Tensor, cache: KVCache) -> torch.Tensor:
         logits = _model_step(model, cond, cache, 0)
         cache.length = cond.shape[1] if idx.shape[1] < bs else 0    # a full window slides next step
         return logits
-    logits = _model_step(model, idx[:, -1:], cache, cache.length)
+    if cache.use_graph:
+        if cache.graph is None:
+            cache.graph = DecodeGraph(model, cache, idx.shape[0], idx.device)
+        logits = cache.graph.step(idx[:, -1:], cache.length)
+    else:
+        logits = _model_step(model, idx[:, -1:], cache, cache.length)
     cache.length += 1
     if cache.length >= bs:
         cache.length = 0

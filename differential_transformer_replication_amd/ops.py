@@ -245,14 +245,19 @@ def rope_rows(src: Tensor, dst: Tensor, table: Tensor) -> None:
     _lib.check(lib.dta_rope(ra, _lib.stream_handle(src.device)))
 
 
-def diff_attention_decode(q: Tensor, k_cache: Tensor, v_cache: Tensor, coef: Tensor, length: int) -> Tensor:
+def diff_attention_decode(q: Tensor, k_cache: Tensor, v_cache: Tensor, coef: Tensor, length: int,
+                          length_dev: Optional[Tensor] = None) -> Tensor:
     """One new query row per (b, h) against the first ``length`` cached keys:
     o = sum_i coef[h,i] softmax(q_i K_i[:length]^T / sqrt(hs)) V[:length].
 
     q: (B, H, N, hs); k_cache: (B, T_cap, H, N, hs); v_cache: (B, T_cap, H, dv)
     (strided views, innermost dim contiguous).  Returns (B, H*dv).  Equals the last
     row of ``diff_attention`` over the same ``length`` positions (the causal mask
-    keeps every key up to the query's own position)."""
+    keeps every key up to the query's own position).
+
+    ``length_dev``: optional device int32 scalar holding the length, read by the
+    kernels, so one captured HIP graph serves every position; ``length`` is then
+    its upper bound (the cache capacity)."""
     lib = _lib.load()
     _require_gpu(q, k_cache, v_cache, coef)
     B, H, N, hs = q.shape
@@ -263,12 +268,17 @@ def diff_attention_decode(q: Tensor, k_cache: Tensor, v_cache: Tensor, coef: Ten
         raise RuntimeError(f"decode length {length} outside [1, {T_cap}]")
     if q.dtype != k_cache.dtype or q.dtype != v_cache.dtype:
         raise RuntimeError("q, k_cache and v_cache must share a dtype")
+    if length_dev is not None:
+        _require_gpu(length_dev)
+        if length_dev.dtype != torch.int32 or length_dev.numel() != 1:
+            raise RuntimeError("length_dev must be one device int32")
     coef = coef.detach().to(torch.float32).contiguous()
     o = torch.empty(B, 1, H, dv, device=q.device, dtype=q.dtype)
     nbytes = lib.dta_attn_decode_workspace_bytes(B, H, N, hs, dv, T_cap)
     ws = torch.empty(nbytes // 4, device=q.device, dtype=torch.float32)
     a = _lib.DecodeArgs(_lib.dtype_code(q.dtype), B, H, N, hs, dv, length, T_cap, 1.0 / math.sqrt(hs),
                         _lib.tensor5(q.unsqueeze(1)), _lib.tensor5(k_cache), _lib.tensor5(v_cache),
-                        _lib.tensor5(o), coef.data_ptr(), ws.data_ptr())
+                        _lib.tensor5(o), coef.data_ptr(), ws.data_ptr(),
+                        None if length_dev is None else length_dev.data_ptr())
     _lib.check(lib.dta_attn_decode(a, _lib.stream_handle(q.device)))
     return o.view(B, H * dv)

@@ -176,6 +176,9 @@ typedef struct dta_attn_decode_args {
   dta_tensor q, k_cache, v_cache, o;
   const float* coef;         /* fp32 [h][i] */
   float* workspace;
+  const int32_t* length_dev; /* optional device int32: the valid length, read by the
+                                kernels (graph replay with a moving position); then
+                                `length` is only its upper bound and sizes the grid */
 } dta_attn_decode_args;
 int dta_attn_decode(const dta_attn_decode_args* a, void* stream);
 size_t dta_attn_decode_workspace_bytes(int32_t B, int32_t H, int32_t n_terms, int32_t head_size, int32_t dv,

@@ -8,7 +8,9 @@
   cache path against a full forward of the same window (the reference's
   generate loop, diff_transformer.py:177-185), through window slides past
   block_size, for DiffTransformer (position table) and AlternatingDiffTransformer
-  (RoPE rows written into the cache); and equal sampled tokens for one seed.
+  (RoPE rows written into the cache), with decode steps both replayed from one
+  captured HIP graph (device-side position) and launched eagerly; and equal
+  sampled tokens for one seed.
 Tolerances (north_star): fp32 max|a-b|/max|b| <= 1e-4, bf16 <= 2e-2.
 """
 import os
@@ -84,8 +86,10 @@ def _models():
     yield "alt3", ND.AlternatingDiffTransformer(97, 256, 2, 2, 24, 0.0, n_terms=3)
 
 
+@pytest.mark.parametrize("graph", ["1", "0"])
 @pytest.mark.parametrize("which", ["diff", "alt3"])
-def test_incremental_logits_match_full_forward(which):
+def test_incremental_logits_match_full_forward(which, graph, monkeypatch):
+    monkeypatch.setenv("DTA_DECODE_GRAPH", graph)          # captured-graph replay and eager steps
     model = dict(_models())[which].to(DEV).eval()
     for p in model.parameters():          # non-zero lambdas so every branch weight differs
         if p.dim() == 1 and p.shape[0] == 64:
@@ -112,3 +116,21 @@ def test_generate_tokens_match_full_recompute(which, monkeypatch):
     slow = model.generate(idx, 30)
     assert fast.shape == (2, 35)
     assert torch.equal(fast, slow)
+
+
+@pytest.mark.parametrize("N,hs,dv", [(2, 64, 128), (3, 64, 128), (2, 48, 96)])
+def test_decode_device_length_matches_host_length(N, hs, dv):
+    """length read on the device (graph replay), grid sized for the capacity."""
+    cap = 1024
+    for L in (1, 255, 256, 257, 700, 1024):
+        got, want = _decode_case(2, 3, N, hs, dv, L, cap, torch.float32, seed=L)
+        g = torch.Generator().manual_seed(L)
+        q = torch.randn(2, cap, 3, N, hs, generator=g).to(DEV)
+        k = torch.randn(2, cap, 3, N, hs, generator=g).to(DEV)
+        v = torch.randn(2, cap, 3, dv, generator=g).to(DEV)
+        coef = (torch.randn(3, N, generator=g) * 0.5).to(DEV)
+        ldev = torch.tensor([L], dtype=torch.int32, device=DEV)
+        a = ops.diff_attention_decode(q[:, L - 1], k, v, coef, cap, length_dev=ldev)
+        b = ops.diff_attention_decode(q[:, L - 1], k, v, coef, L)
+        assert rel_err(a, b) <= 1e-6, (N, hs, L)
+        assert rel_err(got.float(), want) <= 1e-4
