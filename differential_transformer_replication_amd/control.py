@@ -16,7 +16,7 @@ import torch
 import torch.nn as nn
 from torch.nn import functional as F
 
-from . import ops
+from . import kv_cache, ops
 from ._compat import emit_tril_hooks, check_seq_len
 from .Ndiff_transformer import precompute_freqs_cis, apply_rotary_emb, rope_table
 
@@ -161,6 +161,8 @@ class StandardTransformer(nn.Module):
 
     @torch.no_grad()
     def generate(self, idx, max_new_tokens):
+        if kv_cache.enabled(idx, self):                  # KV-cache decode
+            return kv_cache.cached_generate(self, idx, max_new_tokens)
         for _ in range(max_new_tokens):
             logits, _ = self(idx[:, -self.block_size:])
             probs = F.softmax(logits[:, -1, :], dim=-1)

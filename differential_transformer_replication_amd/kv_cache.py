@@ -1,7 +1,7 @@
 """Incremental decoding for ``generate``.
 
 The reference's ``generate`` (diff_transformer.py:177-185; the same loop in
-Ndiff_transformer.py) runs a full forward over ``idx[:, -block_size:]`` for every
+Ndiff_transformer.py, control.py:163-171) runs a full forward over ``idx[:, -block_size:]`` for every
 new token and keeps only the last row of logits.  Here the first call runs the
 prompt once through the fused training kernels (prefill) and keeps every
 layer's K_i / V rows in a KV cache; each further token costs one projection row
@@ -34,8 +34,13 @@ from ._compat import mha_out_scale
 __all__ = ["KVCache", "DecodeGraph", "DevicePosition", "cached_generate", "enabled"]
 
 
-def enabled(idx: torch.Tensor) -> bool:
-    return idx.is_cuda and os.environ.get("DTA_KV_CACHE", "1") != "0"
+def enabled(idx: torch.Tensor, model=None) -> bool:
+    if not idx.is_cuda or os.environ.get("DTA_KV_CACHE", "1") == "0":
+        return False
+    if model is not None:      # a fused plan must exist for the prefill (control: hs 64 / 128)
+        _, _, N, hs, dv, _ = _spec(model.blocks[0])
+        return ops.supported(model.lm_head.weight.dtype, hs, N, dv)
+    return True
 
 
 class KVCache:
@@ -59,31 +64,48 @@ class KVCache:
         return buf
 
 
-def _attention_step(attn, x: torch.Tensor, layer: int, cache: KVCache, pos: int) -> torch.Tensor:
-    """MultiHead(Alternating)DiffAttention.forward for the rows at positions
-    pos .. pos+Tn-1, reading and extending the layer's cache."""
-    H, hs = attn.num_heads, attn.head_size
-    N = getattr(attn, "n_terms", 2)
-    dv = 2 * hs
+def _spec(block):
+    """(attention module, H, N, hs, dv, block_size) of a Block: the differential
+    MHAs (dv = 2hs), or control.py's standard MHA as N = 1, dv = hs."""
+    if hasattr(block, "diff_attn"):
+        a = block.diff_attn
+        return a, a.num_heads, getattr(a, "n_terms", 2), a.head_size, 2 * a.head_size, a.block_size
+    a = block.attn
+    return a, a.num_heads, 1, a.head_size, a.head_size, a.heads[0].block_size
+
+
+def _constants(attn, layer: int, H: int, hs: int, bs: int, device):
+    freqs = None
+    if hasattr(attn.heads[0], "freqs_cis"):
+        from .Ndiff_transformer import rope_table
+        freqs = rope_table(attn.heads[0].freqs_cis, bs, hs).to(device=device, dtype=torch.float32).contiguous()
+    if hasattr(attn, "coefficients"):
+        return attn.packed_weight(), attn.coefficients(layer), freqs
+    # control.py MultiHeadAttention: packed [Q | K | V], one branch of weight 1
+    w = torch.cat([h.query.weight for h in attn.heads] + [h.key.weight for h in attn.heads]
+                  + [h.value.weight for h in attn.heads], 0)
+    return w, torch.ones(H, 1, device=device, dtype=torch.float32), freqs
+
+
+def _attention_step(block, x: torch.Tensor, layer: int, cache: KVCache, pos: int) -> torch.Tensor:
+    """The block's attention forward (MultiHead(Alternating)DiffAttention, or
+    control.py's MultiHeadAttention) for the rows at positions pos .. pos+Tn-1,
+    reading and extending the layer's cache."""
+    attn, H, N, hs, dv, bs = _spec(block)
     consts = cache.consts.get(layer)
     if consts is None:
-        freqs = None
-        if hasattr(attn.heads[0], "freqs_cis"):
-            from .Ndiff_transformer import rope_table
-            freqs = rope_table(attn.heads[0].freqs_cis, attn.block_size, hs).to(
-                device=x.device, dtype=torch.float32).contiguous()
-        consts = (attn.packed_weight(), attn.coefficients(layer), freqs)
+        consts = _constants(attn, layer, H, hs, bs, x.device)
         cache.consts[layer] = consts
     weight, coef, freqs = consts
     rope = freqs is not None
     qkv = F.linear(x, weight)
     B, Tn, W = qkv.shape
     nq = H * N * hs
-    buf = cache.layer(layer, B, attn.block_size, W - nq, qkv)
+    buf = cache.layer(layer, B, bs, W - nq, qkv)
     k_rows = buf[..., :nq].unflatten(-1, (H, N, hs))
     if pos == 0:
         # prefill: the prompt through the training kernels, then cache its K_i / V rows
-        out = ops.diff_attention(qkv, coef, H, N, hs, None if freqs is None else freqs[:Tn])
+        out = ops.diff_attention(qkv, coef, H, N, hs, None if freqs is None else freqs[:Tn], dv)
         src = qkv[..., nq:2 * nq].unflatten(-1, (H, N, hs))
         if rope:
             ops.rope_rows(src, k_rows[:, :Tn], freqs[:Tn])
@@ -107,14 +129,15 @@ def _attention_step(attn, x: torch.Tensor, layer: int, cache: KVCache, pos: int)
         if dev:                                   # graph-replayable: position read on the device
             k_rows.index_copy_(1, pos.idx, k_new)
             v_rows.index_copy_(1, pos.idx, v_new)
-            out = ops.diff_attention_decode(q[:, 0], k_rows, v_rows, coef, attn.block_size, pos.length)
+            out = ops.diff_attention_decode(q[:, 0], k_rows, v_rows, coef, bs, pos.length)
         else:
             k_rows[:, pos:pos + 1].copy_(k_new)
             v_rows[:, pos:pos + 1].copy_(v_new)
             out = ops.diff_attention_decode(q[:, 0], k_rows, v_rows, coef, pos + 1)
         out = out.view(B, 1, H * dv)
-    gn = attn.group_norm
-    out = ops.group_ln_scale(out, gn.weight, gn.bias, gn.eps, mha_out_scale(attn.lambda_init))
+    if hasattr(attn, "group_norm"):
+        gn = attn.group_norm
+        out = ops.group_ln_scale(out, gn.weight, gn.bias, gn.eps, mha_out_scale(attn.lambda_init))
     return attn.dropout(attn.proj(out))
 
 
@@ -166,7 +189,7 @@ def _model_step(model, idx: torch.Tensor, cache: KVCache, pos: int) -> torch.Ten
         rows = pos.idx if isinstance(pos, DevicePosition) else torch.arange(pos, pos + T, device=idx.device)
         x = x + model.position_embedding_table(rows)
     for layer, block in enumerate(model.blocks, 1):
-        x = x + _attention_step(block.diff_attn, block.ln1(x), layer, cache, pos)
+        x = x + _attention_step(block, block.ln1(x), layer, cache, pos)
         x = x + block.ffwd(block.ln2(x))
     return model.lm_head(model.ln_f(x[:, -1:]))[:, -1]
 

@@ -8,7 +8,8 @@
   cache path against a full forward of the same window (the reference's
   generate loop, diff_transformer.py:177-185), through window slides past
   block_size, for DiffTransformer (position table) and AlternatingDiffTransformer
-  (RoPE rows written into the cache), with decode steps both replayed from one
+  (RoPE rows written into the cache) and control.py's StandardTransformer (N=1,
+  dv=hs), with decode steps both replayed from one
   captured HIP graph (device-side position) and launched eagerly; and equal
   sampled tokens for one seed.
 Tolerances (north_star): fp32 max|a-b|/max|b| <= 1e-4, bf16 <= 2e-2.
@@ -24,6 +25,7 @@ from oracle import diffattn_oracle as O
 from differential_transformer_replication_amd import ops, kv_cache
 from differential_transformer_replication_amd import diff_transformer as D
 from differential_transformer_replication_amd import Ndiff_transformer as ND
+from differential_transformer_replication_amd import control as C
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -84,10 +86,12 @@ def _models():
     yield "diff", D.DiffTransformer(vocab_size=97, n_embd=256, n_head=2, n_layer=2, block_size=24, dropout=0.0)
     torch.manual_seed(1)
     yield "alt3", ND.AlternatingDiffTransformer(97, 256, 2, 2, 24, 0.0, n_terms=3)
+    torch.manual_seed(2)
+    yield "ctrl", C.StandardTransformer(97, 256, 4, 2, 24, 0.0)        # N = 1, dv = hs = 64, RoPE
 
 
 @pytest.mark.parametrize("graph", ["1", "0"])
-@pytest.mark.parametrize("which", ["diff", "alt3"])
+@pytest.mark.parametrize("which", ["diff", "alt3", "ctrl"])
 def test_incremental_logits_match_full_forward(which, graph, monkeypatch):
     monkeypatch.setenv("DTA_DECODE_GRAPH", graph)          # captured-graph replay and eager steps
     model = dict(_models())[which].to(DEV).eval()
@@ -105,7 +109,7 @@ def test_incremental_logits_match_full_forward(which, graph, monkeypatch):
             idx = torch.cat([idx, torch.randint(0, 97, (2, 1), generator=g).to(DEV)], dim=1)
 
 
-@pytest.mark.parametrize("which", ["diff", "alt3"])
+@pytest.mark.parametrize("which", ["diff", "alt3", "ctrl"])
 def test_generate_tokens_match_full_recompute(which, monkeypatch):
     model = dict(_models())[which].to(DEV).eval()
     idx = torch.randint(0, 97, (2, 5), generator=torch.Generator().manual_seed(9)).to(DEV)

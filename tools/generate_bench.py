@@ -13,6 +13,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from differential_transformer_replication_amd import diff_transformer as D  # noqa: E402
 from differential_transformer_replication_amd import Ndiff_transformer as ND  # noqa: E402
+from differential_transformer_replication_amd import control as C  # noqa: E402
 
 
 def timed(model, idx, n, cache):
@@ -31,7 +32,9 @@ def main():
     B, prompt, new = 4, 32, 200
     for name, ctor in [("DiffTransformer cfg1", lambda: D.DiffTransformer(12000, 384, 6, 6, 256, 0.0)),
                        ("AlternatingDiffTransformer N=3", lambda: ND.AlternatingDiffTransformer(
-                           12000, 384, 6, 6, 256, 0.0, n_terms=3))]:
+                           12000, 384, 6, 6, 256, 0.0, n_terms=3)),
+                       ("StandardTransformer (control, 6 heads of 64)", lambda: C.StandardTransformer(
+                           12000, 384, 6, 6, 256, 0.0))]:
         torch.manual_seed(0)
         model = ctor().cuda().eval()
         idx = torch.randint(0, 12000, (B, prompt), device="cuda")
