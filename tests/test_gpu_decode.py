@@ -138,3 +138,20 @@ def test_decode_device_length_matches_host_length(N, hs, dv):
         b = ops.diff_attention_decode(q[:, L - 1], k, v, coef, L)
         assert rel_err(a, b) <= 1e-6, (N, hs, L)
         assert rel_err(got.float(), want) <= 1e-4
+
+
+@pytest.mark.parametrize("which", ["diff", "alt3", "ctrl"])
+def test_incremental_logits_bf16_autocast(which):
+    """generate under bf16 autocast: bf16 projections, cache and decode kernel."""
+    model = dict(_models())[which].to(DEV).eval()
+    g = torch.Generator().manual_seed(11)
+    idx = torch.randint(0, 97, (2, 9), generator=g).to(DEV)
+    cache = kv_cache.KVCache()
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        for step in range(20):
+            got = kv_cache.last_logits(model, idx, cache)
+            want = model(idx[:, -model.block_size:])[0][:, -1]
+            assert rel_err(got.float(), want.float()) <= 2e-2, (which, step)
+            idx = torch.cat([idx, torch.randint(0, 97, (2, 1), generator=g).to(DEV)], dim=1)
+        out = model.generate(idx[:, :9], 12)
+    assert out.shape == (2, 21)
