@@ -288,7 +288,15 @@ def decode_bench(args, world, rank):
                    "heads": H, "head_size": hs, "dv": dv, "n_terms": N, "cache_len": L},
         "roofline": {"bound": "hbm", "kernel": "decode_kernel", "achieved": round(nbytes / kms / 1e6, 1),
                      "peak": 8000.0, "unit": "GB/s", "frac": round(nbytes / kms / 1e6 / 8000.0, 4),
-                     "traffic": None, "kernel_ms": round(kms, 5), "alg_bytes": nbytes}}
+                     "traffic": _decode_traffic(B, H, hs, N, L), "kernel_ms": round(kms, 5), "alg_bytes": nbytes}}
+
+
+def _decode_traffic(B, H, hs, N, L):
+    # PMC bytes of the split + combine launches, only for the default decode shape they were measured on
+    if (B, H, hs, N, L) != (8, 16, 64, 2, 4096):
+        return None
+    parts = [_pmc_traffic(k)[0] for k in ("decode_split", "decode_combine")]
+    return None if None in parts else sum(parts)
 
 
 def main():

@@ -11,7 +11,8 @@ import json
 import sys
 from collections import defaultdict
 
-NAMES = {"attn_fwd_kernel": "attn_fwd", "attn_dq_kernel": "attn_bwd_dq", "attn_dkdv_kernel": "attn_bwd_dkdv"}
+NAMES = {"attn_fwd_kernel": "attn_fwd", "attn_dq_kernel": "attn_bwd_dq", "attn_dkdv_kernel": "attn_bwd_dkdv",
+         "decode_split_kernel": "decode_split", "decode_combine_kernel": "decode_combine"}
 
 
 def per_kernel(path, counter):
