@@ -226,7 +226,7 @@ int dta_cast_f32(int32_t dtype, int32_t B, int32_t T, int32_t H, int32_t n_terms
   return status(launch_cast(dtype, src, t5(dst), B, T, H, n_terms, head_size, (hipStream_t)stream));
 }
 
-static int64_t decode_splits(int32_t t_cap) { return (t_cap + 255) / 256; }
+static int64_t decode_splits(int32_t t_cap) { return (t_cap + DTA_DECODE_CHUNK - 1) / DTA_DECODE_CHUNK; }
 
 size_t dta_attn_decode_workspace_bytes(int32_t B, int32_t H, int32_t n_terms, int32_t head_size, int32_t dv,
                                        int32_t t_cap) {

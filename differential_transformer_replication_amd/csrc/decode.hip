@@ -151,7 +151,9 @@ __global__ __launch_bounds__(kThreads) void decode_kernel(DecodeParams p) {
 // rescales the S partials to the global max and applies coef_i / L_i.
 // K rows are read by LPR = HS/8 lanes each (one 16-byte load per lane), V rows
 // by DV/8 lanes each, so every wave-level load is a run of whole rows.
-constexpr int kChunk = 256;
+constexpr int kChunk = DTA_DECODE_CHUNK;        // keys per split workgroup (dta_internal.h)
+constexpr int KPT = kChunk / kThreads;          // keys per thread in the softmax phase
+static_assert(kChunk % kThreads == 0, "chunk must be a multiple of the workgroup");
 
 template <class E, int N, int HS, int DV>
 __global__ __launch_bounds__(kThreads) void decode_split_kernel(DecodeParams p) {
@@ -201,13 +203,22 @@ __global__ __launch_bounds__(kThreads) void decode_split_kernel(DecodeParams p) 
   // phase 2: chunk max / exp / sum per branch (thread = key)
   float m[N], l[N];
 #pragma unroll
-  for (int i = 0; i < N; ++i) m[i] = sc[i][tid];
+  for (int i = 0; i < N; ++i) {
+    m[i] = sc[i][tid];
+#pragma unroll
+    for (int r = 1; r < KPT; ++r) m[i] = fmaxf(m[i], sc[i][tid + r * kThreads]);
+  }
   block_reduce<N, true>(m, red);
 #pragma unroll
   for (int i = 0; i < N; ++i) {
-    const float e = tid < nk ? __expf(sc[i][tid] - m[i]) : 0.f;
-    sc[i][tid] = e;
-    l[i] = e;
+    l[i] = 0.f;
+#pragma unroll
+    for (int r = 0; r < KPT; ++r) {
+      const int j = tid + r * kThreads;
+      const float e = j < nk ? __expf(sc[i][j] - m[i]) : 0.f;
+      sc[i][j] = e;
+      l[i] += e;
+    }
   }
   block_reduce<N, false>(l, red);        // its barriers also publish sc
 

@@ -63,6 +63,10 @@ struct DeltaParams {
   int B, T, H, N, DV;
 };
 
+#ifndef DTA_DECODE_CHUNK
+#define DTA_DECODE_CHUNK 256   // keys per workgroup of the split-key decode plan
+#endif
+
 struct DecodeParams {
   T5 q, k, v, o;       // q/o: one row per (b, h) (st unused); k/v: the cache [b][t][h][i]
   const float* coef;   // [h][i]
