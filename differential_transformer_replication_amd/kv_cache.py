@@ -1,15 +1,17 @@
 """Incremental decoding for ``generate``.
 
 The reference's ``generate`` (diff_transformer.py:177-185; the same loop in
-Ndiff_transformer.py, control.py:163-171) runs a full forward over ``idx[:, -block_size:]`` for every
-new token and keeps only the last row of logits.  Here the first call runs the
+Ndiff_transformer.py and control.py:163-171) runs a full forward over
+``idx[:, -block_size:]`` for every new token and keeps only the last row of
+logits.  Here the first call runs the
 prompt once through the fused training kernels (prefill) and keeps every
 layer's K_i / V rows in a KV cache; each further token costs one projection row
 per layer and one ``dta_attn_decode`` launch (``ops.diff_attention_decode``)
 instead of a T x T recompute.
 
 Positions are absolute within the window (learned position table in
-DiffTransformer, RoPE rows in AlternatingDiffTransformer), so once the sequence
+DiffTransformer, RoPE rows in AlternatingDiffTransformer and the control
+StandardTransformer, which runs as N = 1 with dv = hs), so once the sequence
 outgrows ``block_size`` the window slides, every cached row changes position,
 and the step falls back to the reference's own full recompute of the cropped
 window.  Sampling (softmax of the last logits, ``torch.multinomial``) is the
