@@ -34,6 +34,12 @@
 
 #include <utility>
 
+// dQ kernel: issue every operand read of a branch's S^T ahead of its MFMA chain
+// (1; measured 1% slower at cfg2) or interleave reads with the chain (0, default)
+#ifndef DTA_DQ_AHEAD
+#define DTA_DQ_AHEAD 0
+#endif
+
 namespace dta {
 
 // ------------------------------------------------------------ LDS images ---
@@ -833,6 +839,24 @@ void attn_dq_kernel(BwdParams p) {
             const int Lq = row_lane<QI::ROWB>(lane);
 #pragma unroll
             for (int kb = 0; kb < NKB; ++kb) sa[kb] = f32x16{};
+            if constexpr (DTA_DQ_AHEAD && NSQ * (NKB + 1) <= 12) {
+              // every operand read of this branch's S^T ahead of its MFMA chain (as in attn_fwd_kernel)
+              frag kfr[NKB][NSQ], qfr[NSQ];
+#pragma unroll
+              for (int s = 0; s < NSQ; ++s) {
+                if constexpr (QREG) qfr[s] = qf[i][s];
+                else qfr[s] = *reinterpret_cast<const frag*>(qbase + (Lq ^ (32 * s)));
+#pragma unroll
+                for (int kb = 0; kb < NKB; ++kb)
+                  kfr[kb][s] = *reinterpret_cast<const frag*>(kbase + kb * 32 * KI::ROWB + (Lr ^ (32 * s)));
+              }
+#pragma unroll
+              for (int s = 0; s < NSQ; ++s)
+#pragma unroll
+                for (int kb = 0; kb < NKB; ++kb) sa[kb] = O::mma(kfr[kb][s], qfr[s], sa[kb]);
+              __builtin_amdgcn_sched_group_barrier(0x100, NSQ * (NKB + (QREG ? 0 : 1)), 0);
+              __builtin_amdgcn_sched_group_barrier(0x008, NSQ * NKB, 0);
+            } else {
 #pragma unroll
             for (int s = 0; s < NSQ; ++s) {
               frag qb;
@@ -841,6 +865,7 @@ void attn_dq_kernel(BwdParams p) {
 #pragma unroll
               for (int kb = 0; kb < NKB; ++kb)
                 sa[kb] = O::mma(*reinterpret_cast<const frag*>(kbase + kb * 32 * KI::ROWB + (Lr ^ (32 * s))), qb, sa[kb]);
+            }
             }
           } else {
 #pragma unroll
