@@ -151,16 +151,19 @@ __global__ __launch_bounds__(kThreads) void decode_kernel(DecodeParams p) {
 // rescales the S partials to the global max and applies coef_i / L_i.
 // K rows are read by LPR = HS/8 lanes each (one 16-byte load per lane), V rows
 // by DV/8 lanes each, so every wave-level load is a run of whole rows.
-constexpr int kChunk = DTA_DECODE_CHUNK;        // keys per split workgroup (dta_internal.h)
-constexpr int KPT = kChunk / kThreads;          // keys per thread in the softmax phase
-static_assert(kChunk % kThreads == 0, "chunk must be a multiple of the workgroup");
+// kChunk: keys per split workgroup.  DTA_DECODE_CHUNK (256) sizes the workspace
+// (the most splits); launches with >= kWideGrid workgroups use 2x chunks, which
+// halves the partials (A/B: +4.5% at B=8 H=16 L=32768, slower on smaller grids)
+constexpr int kWideGrid = 8192;
 
-template <class E, int N, int HS, int DV>
+template <class E, int N, int HS, int DV, int kChunk>
 __global__ __launch_bounds__(kThreads) void decode_split_kernel(DecodeParams p) {
   constexpr int LPR = HS / 8;                 // lanes per K row
   constexpr int KPW = 64 / LPR;               // keys per wave per load
   constexpr int VPR = DV / 8;                 // lanes per V row
   constexpr int G = kThreads / VPR;           // V row groups
+  constexpr int KPT = kChunk / kThreads;      // keys per thread in the softmax phase
+  static_assert(kChunk % kThreads == 0, "chunk must be a multiple of the workgroup");
   __shared__ float sc[N][kChunk];
   __shared__ float red[kWaves * N];
   __shared__ float part[G][N][DV + 4];
@@ -262,7 +265,7 @@ __global__ __launch_bounds__(kThreads) void decode_split_kernel(DecodeParams p) 
 
 constexpr int kMaxPartials = 2048;            // S * N per (b, h) for the combine's LDS weights
 
-template <class E, int N>
+template <class E, int N, int kChunk>
 __global__ __launch_bounds__(kThreads) void decode_combine_kernel(DecodeParams p) {
   __shared__ float wgt[kMaxPartials];          // [s][i] = coef_i / L_i * exp(m_is - M_i)
   __shared__ float red[kWaves * N];
@@ -303,9 +306,17 @@ __global__ __launch_bounds__(kThreads) void decode_combine_kernel(DecodeParams p
 }
 
 template <class E, int N, int HS, int DV>
-int split_launch(const DecodeParams& p, hipStream_t st) {
-  hipLaunchKernelGGL((decode_split_kernel<E, N, HS, DV>), dim3(p.S, p.H, p.B), dim3(kThreads), 0, st, p);
-  hipLaunchKernelGGL((decode_combine_kernel<E, N>), dim3(p.H, p.B), dim3(kThreads), 0, st, p);
+int split_launch(const DecodeParams& p0, hipStream_t st) {
+  constexpr int C = DTA_DECODE_CHUNK;
+  if ((int64_t)p0.S * p0.H * p0.B >= kWideGrid) {
+    DecodeParams p = p0;
+    p.S = (p0.S + 1) / 2;                      // same partial layout, half the rows used
+    hipLaunchKernelGGL((decode_split_kernel<E, N, HS, DV, 2 * C>), dim3(p.S, p.H, p.B), dim3(kThreads), 0, st, p);
+    hipLaunchKernelGGL((decode_combine_kernel<E, N, 2 * C>), dim3(p.H, p.B), dim3(kThreads), 0, st, p);
+    return (int)hipGetLastError();
+  }
+  hipLaunchKernelGGL((decode_split_kernel<E, N, HS, DV, C>), dim3(p0.S, p0.H, p0.B), dim3(kThreads), 0, st, p0);
+  hipLaunchKernelGGL((decode_combine_kernel<E, N, C>), dim3(p0.H, p0.B), dim3(kThreads), 0, st, p0);
   return (int)hipGetLastError();
 }
 

@@ -155,3 +155,28 @@ def test_incremental_logits_bf16_autocast(which):
             idx = torch.cat([idx, torch.randint(0, 97, (2, 1), generator=g).to(DEV)], dim=1)
         out = model.generate(idx[:, :9], 12)
     assert out.shape == (2, 21)
+
+
+def _torch_decode_ref(q, k, v, coef, L):
+    """fp32 torch restatement of one decode row (softmax per branch, signed sum, @V)."""
+    s = torch.einsum("bhid,bthid->bhit", q.float(), k[:, :L].float()) / q.shape[-1] ** 0.5
+    a = torch.softmax(s, dim=-1) * coef.float()[None, :, :, None]
+    return torch.einsum("bht,bthe->bhe", a.sum(2), v[:, :L].float())
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_decode_wide_grid_plan(dtype):
+    """B*H*ceil(L/256) >= 8192 switches to 512-key chunks; also with a device length."""
+    B, H, N, hs, cap = 4, 16, 2, 64, 32768
+    g = torch.Generator(device=DEV).manual_seed(21)
+    k = torch.randn(B, cap, H, N, hs, device=DEV, generator=g).to(dtype)
+    v = torch.randn(B, cap, H, 2 * hs, device=DEV, generator=g).to(dtype)
+    q = torch.randn(B, H, N, hs, device=DEV, generator=g).to(dtype)
+    coef = torch.tensor([[1.0, -0.7]] * H, device=DEV)
+    for L in (cap, cap - 100, 30001):
+        want = _torch_decode_ref(q, k, v, coef, L)
+        got = ops.diff_attention_decode(q, k, v, coef, L).view(B, H, -1)
+        assert rel_err(got.float(), want) <= TOL[dtype], (dtype, L)
+        ldev = torch.tensor([L], dtype=torch.int32, device=DEV)
+        got2 = ops.diff_attention_decode(q, k, v, coef, cap, length_dev=ldev).view(B, H, -1)
+        assert rel_err(got2.float(), want) <= TOL[dtype], (dtype, L, "device length")
