@@ -240,8 +240,10 @@ int dta_attn_decode(const dta_attn_decode_args* a, void* stream) {
   if (a->head_size % 8 || a->head_size > 128 || a->n_terms > 4 || a->dv > 256) return DTA_ERR_UNSUPPORTED;
   if (a->length < 1 || a->t_cap < a->length) return DTA_ERR_INVALID;
   if ((int64_t)a->B * a->H == 0) return DTA_OK;
+  // every operand is read or written by 16-byte vector accesses: full alignment checks on all four
   if (!ok_tensor(a->q, a->dtype, true) || !ok_tensor(a->k_cache, a->dtype, true) ||
-      !a->v_cache.ptr || !a->o.ptr || !a->coef || !aligned_ptr(a->workspace))
+      !ok_tensor(a->v_cache, a->dtype, false) || !ok_tensor(a->o, a->dtype, false) || !a->coef ||
+      !aligned_ptr(a->workspace))
     return DTA_ERR_INVALID;
   DecodeParams p{};
   p.q = t5(a->q); p.k = t5(a->k_cache); p.v = t5(a->v_cache); p.o = t5(a->o);

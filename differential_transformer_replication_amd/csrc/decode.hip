@@ -69,13 +69,20 @@ __device__ __forceinline__ void block_reduce(float (&v)[NB], float* red) {
   __syncthreads();
 }
 
+// The valid length: the device value when given, clamped to [0, L] (L = the host
+// upper bound the grid and workspace were sized for), so a bad device length can
+// never index past the cache, the workspace or the combine's LDS weights.
+__device__ __forceinline__ int clamp_len(const DecodeParams& p) {
+  return p.Ldev ? min(max(*p.Ldev, 0), p.L) : p.L;
+}
+
 template <class E, int N>
 __global__ __launch_bounds__(kThreads) void decode_kernel(DecodeParams p) {
   __shared__ float qs[N * 128];
   __shared__ float red[kWaves * N];
   __shared__ float part[kThreads];
   const int h = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
-  const int HS = p.HS, DV = p.DV, L = p.Ldev ? *p.Ldev : p.L;
+  const int HS = p.HS, DV = p.DV, L = clamp_len(p);
   const E* gq = reinterpret_cast<const E*>(p.q.p) + b * p.q.sb + h * p.q.sh;
   for (int x = tid; x < N * HS; x += kThreads) qs[x] = (float)gq[(x / HS) * p.q.si + x % HS];
   __syncthreads();
@@ -169,7 +176,7 @@ __global__ __launch_bounds__(kThreads) void decode_split_kernel(DecodeParams p) 
   __shared__ float part[G][N][DV + 4];
   const int s = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int j0 = s * kChunk, L = p.Ldev ? *p.Ldev : p.L;
+  const int j0 = s * kChunk, L = clamp_len(p);
   if (j0 >= L) return;                         // grid sized for an upper bound (uniform exit)
   const int nk = min(kChunk, L - j0);
 
@@ -271,7 +278,7 @@ __global__ __launch_bounds__(kThreads) void decode_combine_kernel(DecodeParams p
   __shared__ float red[kWaves * N];
   const int h = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
   const int64_t row0 = ((int64_t)b * p.H + h) * p.S;       // partial stride: the launch's S
-  const int S = p.Ldev ? (*p.Ldev + kChunk - 1) / kChunk : p.S;  // chunks written this call
+  const int S = min((clamp_len(p) + kChunk - 1) / kChunk, p.S);  // chunks written this call
   const float* ml = p.ml + row0 * N * 2;
   float M[N], Ls[N];
 #pragma unroll
@@ -305,18 +312,27 @@ __global__ __launch_bounds__(kThreads) void decode_combine_kernel(DecodeParams p
   }
 }
 
+// Chunk size is chosen from the cache capacity (ldw = t_cap), not from the
+// current length, so the eager path (length = pos + 1) and the graph path
+// (length = t_cap, device length) launch the same chunks and reduce in the same
+// order: their outputs are bitwise equal at every position.
 template <class E, int N, int HS, int DV>
 int split_launch(const DecodeParams& p0, hipStream_t st) {
   constexpr int C = DTA_DECODE_CHUNK;
-  if ((int64_t)p0.S * p0.H * p0.B >= kWideGrid) {
-    DecodeParams p = p0;
-    p.S = (p0.S + 1) / 2;                      // same partial layout, half the rows used
+  const int64_t s_cap = (p0.ldw + C - 1) / C;
+  const bool wide = s_cap * p0.H * p0.B >= kWideGrid;
+  const int chunk = wide ? 2 * C : C;
+  // the combine keeps one LDS weight per (chunk, branch): gate on the chunk actually launched
+  if (((int64_t)p0.ldw + chunk - 1) / chunk * N > kMaxPartials) return 1;
+  DecodeParams p = p0;
+  p.S = (p0.L + chunk - 1) / chunk;            // same partial layout as C-key chunks, fewer rows used
+  if (wide) {
     hipLaunchKernelGGL((decode_split_kernel<E, N, HS, DV, 2 * C>), dim3(p.S, p.H, p.B), dim3(kThreads), 0, st, p);
     hipLaunchKernelGGL((decode_combine_kernel<E, N, 2 * C>), dim3(p.H, p.B), dim3(kThreads), 0, st, p);
-    return (int)hipGetLastError();
+  } else {
+    hipLaunchKernelGGL((decode_split_kernel<E, N, HS, DV, C>), dim3(p.S, p.H, p.B), dim3(kThreads), 0, st, p);
+    hipLaunchKernelGGL((decode_combine_kernel<E, N, C>), dim3(p.H, p.B), dim3(kThreads), 0, st, p);
   }
-  hipLaunchKernelGGL((decode_split_kernel<E, N, HS, DV, C>), dim3(p0.S, p0.H, p0.B), dim3(kThreads), 0, st, p0);
-  hipLaunchKernelGGL((decode_combine_kernel<E, N, C>), dim3(p0.H, p0.B), dim3(kThreads), 0, st, p0);
   return (int)hipGetLastError();
 }
 
@@ -332,7 +348,7 @@ int split_dispatch(const DecodeParams& p, hipStream_t st) {
 
 template <class E>
 int decode_launch(const DecodeParams& p, hipStream_t st) {
-  if (p.ml && p.S * p.N <= kMaxPartials) {
+  if (p.ml) {
     int e = 1;
     switch (p.N) {
       case 1: e = split_dispatch<E, 1>(p, st); break;

@@ -162,11 +162,16 @@ int dta_rope(const dta_rope_args* a, void* stream);
  * is the query's own position, so the causal mask keeps every cached key).
  * q: [b][.][h][i][d] (st ignored), k_cache [b][t][h][i][d], v_cache [b][t][h][e],
  * o [b][.][h][e] (st ignored).  head_size % 8 == 0, head_size <= 128,
- * n_terms <= 4, dv <= 256.  workspace: fp32, dta_attn_decode_workspace_bytes
- * (covers both plans: a split-key plan -- 256-key chunks scored by separate
+ * n_terms <= 4, dv <= 256; every tensor 16-byte aligned with strides that are
+ * multiples of 16 bytes.  workspace: fp32, dta_attn_decode_workspace_bytes
+ * (covers both plans).  Plans: a split-key plan -- key chunks scored by separate
  * workgroups, then one combine launch -- for (head_size, dv) in {(32,64),
- * (64,128), (128,256)} and, with n_terms = 1, dv = head_size in {64, 128};
- * a single-pass workgroup per (b, h) otherwise). */
+ * (64,128), (128,256)} and, with n_terms = 1, dv = head_size in {64, 128}; a
+ * single-pass workgroup per (b, h) otherwise.  The split plan uses 256-key
+ * chunks, or 512-key chunks when ceil(t_cap/256) * H * B >= 8192 workgroups;
+ * the choice depends on t_cap only, so calls with the same t_cap reduce in the
+ * same order whatever their length.  It is used while ceil(t_cap/chunk) *
+ * n_terms <= 2048 (the combine's LDS weights). */
 typedef struct dta_attn_decode_args {
   int32_t dtype;
   int32_t B, H, n_terms, head_size, dv;
@@ -178,7 +183,9 @@ typedef struct dta_attn_decode_args {
   float* workspace;
   const int32_t* length_dev; /* optional device int32: the valid length, read by the
                                 kernels (graph replay with a moving position); then
-                                `length` is only its upper bound and sizes the grid */
+                                `length` is only its upper bound and sizes the grid.
+                                Precondition 1 <= *length_dev <= length <= t_cap; the
+                                kernels clamp it to [0, length] */
 } dta_attn_decode_args;
 int dta_attn_decode(const dta_attn_decode_args* a, void* stream);
 size_t dta_attn_decode_workspace_bytes(int32_t B, int32_t H, int32_t n_terms, int32_t head_size, int32_t dv,

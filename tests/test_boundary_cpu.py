@@ -53,6 +53,29 @@ def test_invalid_args_rejected_without_gpu():
     assert lib.dta_attn_fwd(None, None) == -1
 
 
+def test_decode_misaligned_views_rejected_without_gpu():
+    """dta_attn_decode checks alignment of all four operands (16-byte vector
+    accesses); a misaligned V or O view is refused before anything launches."""
+    lib = _lib.load()
+    base = 0x10000                                      # fake, 16-byte aligned device addresses
+    a = _lib.DecodeArgs()
+    a.dtype, a.B, a.H, a.n_terms, a.head_size, a.dv = 0, 1, 2, 2, 64, 128
+    a.length, a.t_cap, a.scale = 4, 8, 0.125
+    ok = lambda p, st: _lib.DtaTensor(p, 8 * st, st, 128, 64)
+    a.q, a.k_cache = ok(base, 512), ok(base + 4096, 512)
+    a.coef, a.workspace = base + 8192, base + 8192 + 64
+    a.v_cache = _lib.DtaTensor(base + 2, 8 * 256, 256, 128, 0)         # base off by one element
+    a.o = ok(base, 256)
+    assert lib.dta_attn_decode(a, None) == -1
+    a.v_cache = _lib.DtaTensor(base, 8 * 257, 257, 128, 0)             # row stride not a 16-byte multiple
+    assert lib.dta_attn_decode(a, None) == -1
+    a.v_cache = _lib.DtaTensor(base, 8 * 256, 256, 128, 0)
+    a.o = _lib.DtaTensor(base + 6, 256, 256, 128, 0)                  # misaligned output
+    assert lib.dta_attn_decode(a, None) == -1
+    a.o = _lib.DtaTensor(None, 256, 256, 128, 0)
+    assert lib.dta_attn_decode(a, None) == -1
+
+
 def _cases(golden, prefix):
     return sorted({f.split("/")[0] for f in golden.files if f.startswith(prefix)})
 
