@@ -16,8 +16,22 @@ bracketing its launches inside the timed region.  ``cpu_baseline`` times the CPU
 oracle (the reference's algorithm op for op: per-head loop, materialised T x T
 maps, fp32) on a bounded sample on this host.
 
+The kernel line also carries:
+  ``train``        BASELINE configs[3] -- the ~350M DiffTransformer DP training
+                   step (bucketed RCCL all-reduce overlapped with backward) at
+                   this run's world size: whole-job train tokens/s, so the 1/2/4/8
+                   GPU lines give the train scaling curve (``--train-steps 0`` skips);
+  ``hbm_kernels``  the HBM-bound norm / RoPE kernels at their BASELINE shapes
+                   (GroupLayerNorm fwd/bwd at cfg2's 32768 x 2048, RoPE at cfg3),
+                   HIP-event times and GB/s against 8 TB/s.
+
 ``--mode train``: data-parallel training tokens/s of a reference-architecture
 model (see differential_transformer_replication_amd/train.py).
+
+Launch: ``torchrun --nproc-per-node N ... bench.py --gpus N`` (one rank per GPU,
+RCCL), or plain ``python bench.py --gpus N``, which spawns the N ranks itself
+before anything touches the GPU.  ``--device cpu`` is a CPU/gloo dry run of the
+multi-rank path (train leg only, a small control model).
 """
 from __future__ import annotations
 
@@ -38,15 +52,17 @@ METRIC = "diff-attn fwd+bwd TFLOP/s (% MFMA peak); train tokens/sec at 1/2/4/8 G
 PEAK_BF16_TFLOPS = 2516.6          # 256 CU x 2.4 GHz x 4096 flop/clk/CU (dense, MI355X_MICROARCH.md)
 
 
-def _dist():
+def _dist(device="cuda"):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if device == "cpu":
+        if world > 1:
+            dist.init_process_group("gloo")
+        return world, rank, local
+    torch.cuda.set_device(local)
     if world > 1:
-        torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(local)
     return world, rank, local
 
 
@@ -65,26 +81,45 @@ def _max_over_ranks(x: float, world: int) -> float:
     return float(t.item())
 
 
+def _host_threads() -> int:
+    """Host threads this process may use: OMP_NUM_THREADS when the launcher sets it
+    (the GPU box sets its CPU share, 16, there), else the CPUs in our affinity mask
+    (os.cpu_count() reports the whole machine on the box)."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
 def cpu_baseline(T=4096, H=16, hs=64, reps=2):
     """Oracle (reference algorithm, eager fp32, per-head loop) on the host CPU.
     Bounded sample: B=1, H=16 at the full T; heads and batch entries are
-    independent so the rate per FLOP carries to B=8."""
+    independent so the rate per FLOP carries to B=8.  Inputs are drawn before the
+    timed region; the oracle keeps the reference's persistent causal mask
+    (a ``tril`` built once, compared per call: diff_transformer.py:31,61-62)."""
     from oracle import diffattn_oracle as orc
-    threads = max(1, min(16, os.cpu_count() or 1))
+    threads = _host_threads()
     torch.set_num_threads(threads)
     g = torch.Generator().manual_seed(0)
     dv = 2 * hs
+    heads = []
+    for _h in range(H):
+        q = [torch.randn(1, T, hs, generator=g, requires_grad=True) for _ in range(2)]
+        k = [torch.randn(1, T, hs, generator=g, requires_grad=True) for _ in range(2)]
+        v = torch.randn(1, T, dv, generator=g, requires_grad=True)
+        heads.append((q, k, v, torch.randn(1, T, dv, generator=g)))
+    lam = torch.tensor(0.47, requires_grad=True)
+    orc.causal_softmax(heads[0][0][0][:, :8].detach(), heads[0][1][0][:, :8].detach(), 0.125)   # warm
     ts = []
     for _ in range(reps):
         t0 = time.perf_counter()
-        for _h in range(H):
-            q = [torch.randn(1, T, hs, generator=g, requires_grad=True) for _ in range(2)]
-            k = [torch.randn(1, T, hs, generator=g, requires_grad=True) for _ in range(2)]
-            v = torch.randn(1, T, dv, generator=g, requires_grad=True)
-            lam = torch.tensor(0.47, requires_grad=True)
+        for q, k, v, do in heads:
             coef = torch.stack([torch.ones(()), -lam])
             out = orc.diff_core(q, k, v, coef)
-            out.backward(torch.randn(1, T, dv, generator=g))
+            out.backward(do)
         ts.append(time.perf_counter() - t0)
     f_fwd, f_bwd = orc.flops_attention(1, H, T, hs, dv, 2)
     sec = sum(ts) / len(ts)
@@ -92,20 +127,33 @@ def cpu_baseline(T=4096, H=16, hs=64, reps=2):
             "kind": "port",
             "sample": f"CPU oracle (reference algorithm op for op, eager fp32, per-head loop, materialised "
                       f"T x T maps) fwd+bwd of B=1 H={H} T={T} hs={hs} N=2, mean of {reps}; "
-                      f"{sec:.2f} s per sample; rate per algorithmic FLOP, same FLOP count as the GPU step"}
+                      f"{sec:.2f} s per sample; rate per algorithmic FLOP, same FLOP count as the GPU step; "
+                      f"fidelity vs the reference itself: profiles/r02_cpu_fidelity.json"}
 
 
-def _pmc_traffic(kernel):
-    """HBM bytes per launch of ``kernel`` from the newest committed PMC summary
-    (profiles/*_pmc_traffic.json, written from separate rocprofv3 --pmc FETCH_SIZE /
-    WRITE_SIZE passes of this same command, FETCH_SIZE doubled per the gfx950
-    correction).  (None, None) when no summary exists."""
+DEFAULT_SHAPE = "B8_H16_hs64_N2_T4096_dv128"       # cfg2, the default kernel workload
+
+
+def shape_key(B, H, hs, N, T, dv) -> str:
+    return f"B{B}_H{H}_hs{hs}_N{N}_T{T}_dv{dv}"
+
+
+def _pmc_traffic(kernel, shape=DEFAULT_SHAPE):
+    """HBM bytes per launch of ``kernel`` at workload ``shape`` from the newest
+    committed PMC summary for that shape (profiles/*_pmc_traffic.json, written
+    from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE doubled
+    per the gfx950 correction).  Summaries without a "shape" field were all taken
+    on the default cfg2 command.  (None, None) when no summary matches."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))   # rNN_vM: newest last
     for f in reversed(files):
         try:
             with open(f) as fh:
-                k = json.load(fh)["kernels"].get(kernel)
+                d = json.load(fh)
+            legacy = ("decode_" if kernel.startswith("decode") else "") + DEFAULT_SHAPE
+            if d.get("shape", legacy) != shape:
+                continue
+            k = d["kernels"].get(kernel)
         except (OSError, ValueError, KeyError):
             continue
         if k:
@@ -220,7 +268,7 @@ def kernel_bench(args, world, rank):
     achieved = kernels[dom]["alg_tflops"]
     traffic, traffic_src = args.traffic, None
     if traffic is None:
-        traffic, traffic_src = _pmc_traffic(dom)
+        traffic, traffic_src = _pmc_traffic(dom, shape_key(B, H, hs, N, T, dv))
     cfg2 = (B, H, hs, N, T) == (8, 16, 64, 2, 4096)
     workload = ("cfg2: fused N=2 diff-attention core fwd+bwd (BASELINE configs[1])" if cfg2 else
                 f"diff-attention core fwd+bwd B={B} H={H} hs={hs} N={N} T={T}")
@@ -295,8 +343,133 @@ def _decode_traffic(B, H, hs, N, L):
     # PMC bytes of the split + combine launches, only for the default decode shape they were measured on
     if (B, H, hs, N, L) != (8, 16, 64, 2, 4096):
         return None
-    parts = [_pmc_traffic(k)[0] for k in ("decode_split", "decode_combine")]
+    parts = [_pmc_traffic(k, "decode_" + shape_key(B, H, hs, N, L, 2 * hs))[0] for k in ("decode_split", "decode_combine")]
     return None if None in parts else sum(parts)
+
+
+def hbm_bench(reps=20):
+    """The HBM-bound kernels around the attention core, at BASELINE shapes, timed
+    with HIP events on the launch stream (median of ``reps``):
+      ln_fwd / ln_bwd  GroupLayerNorm x0.2 (diff_transformer.py:15-20, 90-91) at cfg2:
+                       B*T = 32768 rows x C' = H*dv = 2048, bf16;
+                       algorithmic bytes fwd 2*rows*C'*2 (read x, write y),
+                       bwd 3*rows*C'*2 (read x and dy, write dx);
+      rope             interleaved-pair RoPE of every Q_i/K_i (Ndiff_transformer.py:11-22)
+                       at cfg3: B=16, T=2048, 2H=12 (Q and K of H=6 heads), N=3, hs=64,
+                       bf16; bytes 2 * elements * 2 (read, write; the fp32 table is
+                       T*hs*4 and stays in cache)."""
+    from differential_transformer_replication_amd import ops, _lib
+    dev = torch.device("cuda", torch.cuda.current_device())
+    g = torch.Generator(device=dev).manual_seed(3)
+    out = {}
+    rows, C = 8 * 4096, 16 * 128
+    x = torch.randn(rows, C, device=dev, dtype=torch.bfloat16, generator=g)
+    w = torch.ones(C, device=dev) + 0.1 * torch.randn(C, device=dev, generator=g)
+    b = 0.1 * torch.randn(C, device=dev, generator=g)
+    dy = torch.randn(rows, C, device=dev, dtype=torch.bfloat16, generator=g)
+
+    def timed(fn):
+        for _ in range(3):
+            fn()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+        for e0, e1 in ev:
+            e0.record()
+            fn()
+            e1.record()
+        torch.cuda.synchronize()
+        ts = sorted(a.elapsed_time(b_) for a, b_ in ev)
+        return ts[len(ts) // 2]
+
+    lib = _lib.load()
+    stream = _lib.stream_handle(dev)
+    y = torch.empty_like(x)
+    mean = torch.empty(rows, device=dev)
+    rstd = torch.empty(rows, device=dev)
+    dx = torch.empty_like(x)
+    dw = torch.zeros(C, device=dev)
+    db = torch.zeros(C, device=dev)
+    fa = _lib.LnArgs(_lib.DTA_BF16, rows, C, 1e-5, 0.2, x.data_ptr(), C, y.data_ptr(), C, w.data_ptr(),
+                     b.data_ptr(), mean.data_ptr(), rstd.data_ptr(), None, 0, None, 0, None, None)
+    ba = _lib.LnArgs(_lib.DTA_BF16, rows, C, 1e-5, 0.2, x.data_ptr(), C, None, 0, w.data_ptr(), None,
+                     mean.data_ptr(), rstd.data_ptr(), dy.data_ptr(), C, dx.data_ptr(), C, dw.data_ptr(),
+                     db.data_ptr())
+    ms_f = timed(lambda: _lib.check(lib.dta_ln_fwd(fa, stream)))
+    ms_b = timed(lambda: _lib.check(lib.dta_ln_bwd(ba, stream)))     # dw/db accumulate: values unused
+    for name, ms, nbytes in (("ln_fwd", ms_f, 2 * rows * C * 2), ("ln_bwd", ms_b, 3 * rows * C * 2)):
+        out[name] = {"us": round(ms * 1e3, 2), "alg_bytes": nbytes, "GBps": round(nbytes / ms / 1e6, 1),
+                     "frac_of_8TBps": round(nbytes / ms / 1e6 / 8000.0, 4)}
+    B, T, H2, N, hs = 16, 2048, 12, 3, 64
+    src = torch.randn(B, T, H2, N, hs, device=dev, dtype=torch.bfloat16, generator=g)
+    dst = torch.empty_like(src)
+    from differential_transformer_replication_amd.Ndiff_transformer import precompute_freqs_cis
+    table = torch.view_as_real(precompute_freqs_cis(hs, T)).to(dev).contiguous()
+    ms_r = timed(lambda: ops.rope_rows(src, dst, table))
+    nbytes = 2 * src.numel() * 2
+    out["rope"] = {"us": round(ms_r * 1e3, 2), "alg_bytes": nbytes, "GBps": round(nbytes / ms_r / 1e6, 1),
+                   "frac_of_8TBps": round(nbytes / ms_r / 1e6 / 8000.0, 4),
+                   "shape": f"B={B} T={T} 2H={H2} N={N} hs={hs} bf16"}
+    del x, y, dy, dx, src, dst
+    return out
+
+
+def train_leg(args, world, rank):
+    """BASELINE configs[3] DP training step (cfg4) at this run's world size."""
+    from differential_transformer_replication_amd.train import train_bench
+    targs = argparse.Namespace(steps=args.train_steps, warmup=args.train_warmup, model="diff",
+                               n_terms=args.n_terms, device=args.device)
+    r = train_bench(targs, world, rank)
+    keep = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "final_loss", "config",
+            "model_tflops", "mfu")
+    return {k: r[k] for k in keep if k in r}
+
+
+def run(args):
+    world, rank, local = _dist(args.device)
+    if args.device == "cpu":
+        # CPU / gloo dry run of the multi-rank path: the train leg on a small control model
+        from differential_transformer_replication_amd.train import train_bench
+        targs = argparse.Namespace(steps=args.steps, warmup=args.warmup, model="cpu-dry", n_terms=args.n_terms,
+                                   device="cpu")
+        res = train_bench(targs, world, rank)
+        res["cpu_baseline"] = None
+    elif args.mode == "kernel":
+        res = kernel_bench(args, world, rank)
+        if rank == 0 and args.hbm:
+            res["hbm_kernels"] = hbm_bench()
+        if args.train_steps > 0:
+            torch.cuda.empty_cache()
+            res["train"] = train_leg(args, world, rank)
+    elif args.mode == "decode":
+        res = decode_bench(args, world, rank)
+    else:
+        from differential_transformer_replication_amd.train import train_bench
+        res = train_bench(args, world, rank)
+    if rank == 0:
+        default_kernel = args.mode == "kernel" and args.device == "cuda" and (
+            args.batch, args.heads, args.head_size, args.n_terms, args.seq) == (8, 16, 64, 2, 4096)
+        if args.cpu_baseline == "auto" and world == 1 and default_kernel:
+            res["cpu_baseline"] = cpu_baseline()
+        elif "cpu_baseline" not in res:
+            res["cpu_baseline"] = None
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def _rank_main(rank, args, world, port):
+    # a spawned rank: the same environment torchrun would give it
+    os.environ.update({"RANK": str(rank), "LOCAL_RANK": str(rank), "WORLD_SIZE": str(world),
+                       "LOCAL_WORLD_SIZE": str(world), "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    run(args)
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
 
 
 def main():
@@ -305,6 +478,8 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--mode", choices=["kernel", "train", "decode"], default="kernel")
+    ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
+                    help="cpu: gloo dry run of the multi-rank path (train leg on a small control model)")
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--seq", type=int, default=4096)
     ap.add_argument("--heads", type=int, default=16)
@@ -314,29 +489,25 @@ def main():
                     help="kernel mode: also time control.py standard attention at equal F_fwd (BASELINE configs[4])")
     ap.add_argument("--model", choices=["diff", "ndiff"], default="diff",
                     help="train mode: cfg4 DiffTransformer (diff) or cfg3 AlternatingDiffTransformer (ndiff)")
+    ap.add_argument("--train-steps", type=int, default=8,
+                    help="kernel mode: timed steps of the cfg4 DP training leg (0 = skip)")
+    ap.add_argument("--train-warmup", type=int, default=3)
+    ap.add_argument("--no-hbm", dest="hbm", action="store_false", help="kernel mode: skip the LN / RoPE timings")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--traffic", type=float, default=None,
                     help="HBM bytes per dominant-kernel launch from rocprofv3 PMC (profiles/)")
     args = ap.parse_args()
-    world, rank, local = _dist()
-    if args.mode == "kernel":
-        res = kernel_bench(args, world, rank)
-    elif args.mode == "decode":
-        res = decode_bench(args, world, rank)
-    else:
-        from differential_transformer_replication_amd.train import train_bench
-        res = train_bench(args, world, rank)
-    if rank == 0:
-        default_kernel = args.mode == "kernel" and (args.batch, args.heads, args.head_size, args.n_terms,
-                                                     args.seq) == (8, 16, 64, 2, 4096)
-        if args.cpu_baseline == "auto" and world == 1 and default_kernel:
-            res["cpu_baseline"] = cpu_baseline()
-        else:
-            res["cpu_baseline"] = None
-        print(json.dumps(res), flush=True)
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None and int(env_world) != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world}", file=sys.stderr)
+        sys.exit(2)
+    if args.gpus > 1 and env_world is None:
+        # spawn the ranks here, before this process touches the GPU
+        import torch.multiprocessing as mp
+        mp.start_processes(_rank_main, args=(args, args.gpus, _free_port()), nprocs=args.gpus, join=True,
+                           start_method="spawn")
+        return
+    run(args)
 
 
 if __name__ == "__main__":

@@ -287,51 +287,95 @@ CFG3 = dict(model="ndiff", vocab_size=12000, n_embd=768, n_head=6, n_layer=10, b
             micro_batch_size=16)
 
 
+# CPU / gloo dry run of the multi-rank path (bench.py --device cpu): a small control model
+CPU_DRY = dict(model="control", vocab_size=256, n_embd=64, n_head=2, n_layer=2, block_size=32, dropout=0.0,
+               micro_batch_size=4, device="cpu", dtype="fp32")
+
+PEAK_BF16_TFLOPS = 2516.6          # MI355X dense bf16 MFMA peak (MI355X_MICROARCH.md)
+
+
+def model_flops_per_token(model: torch.nn.Module, cfg: TrainingConfig) -> float:
+    """Training FLOPs per token: 6 x (parameters in matmuls: everything but the
+    token / position embedding tables) + the attention core's causal-halved
+    fwd+bwd matmuls per token, 3 * H * T * (N*hs + dv) per layer."""
+    skip = 0
+    for name, p in model.named_parameters():
+        if name.endswith("tok_emb.weight") or name.endswith("pos_emb.weight") or \
+                name.endswith("token_embedding_table.weight") or name.endswith("position_embedding_table.weight"):
+            skip += p.numel()
+    dense = sum(p.numel() for p in model.parameters()) - skip
+    if cfg.model == "control":
+        H, hs, N, dv = cfg.n_head * 2, cfg.n_embd // (cfg.n_head * 2), 1, cfg.n_embd // (cfg.n_head * 2)
+    else:
+        H, hs = cfg.n_head, cfg.n_embd // (2 * cfg.n_head)
+        N, dv = (cfg.n_terms if cfg.model == "ndiff" else 2), 2 * hs
+    attn = 3.0 * H * cfg.block_size * (N * hs + dv) * cfg.n_layer
+    return 6.0 * dense + attn
+
+
 def train_bench(args, world, rank):
     """bench.py --mode train: BASELINE configs[3] -- ~350M DiffTransformer
     (12000, 1024, 8, 20, 2048), micro-batch 16 x 2048 per GPU, bf16 autocast,
     AdamW, DP all-reduce.  value = tokens/s over all ranks.  With --model ndiff:
     BASELINE configs[2] -- AlternatingDiffTransformer(12000, 768, 6, 10, 2048,
-    n_terms=--n-terms), micro-batch 16 x 2048."""
+    n_terms=--n-terms), micro-batch 16 x 2048.  model "cpu-dry": a small control
+    model on CPU over gloo (bench.py --device cpu), fp32."""
     arch = getattr(args, "model", "diff")
-    base = CFG3 if arch == "ndiff" else CFG4
-    extra = {"n_terms": args.n_terms} if arch == "ndiff" else {}
-    cfg = TrainingConfig(**base, **extra, warmup_iters=100, max_iters=10_000, dtype="bf16")
-    dev = torch.device("cuda", torch.cuda.current_device())
+    if arch == "cpu-dry":
+        cfg = TrainingConfig(**CPU_DRY, warmup_iters=10, max_iters=1000)
+        dev = torch.device("cpu")
+    else:
+        base = CFG3 if arch == "ndiff" else CFG4
+        extra = {"n_terms": args.n_terms} if arch == "ndiff" else {}
+        cfg = TrainingConfig(**base, **extra, warmup_iters=100, max_iters=10_000, dtype="bf16")
+        dev = torch.device("cuda", torch.cuda.current_device())
+    cuda = dev.type == "cuda"
+
+    def sync():
+        if cuda:
+            torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+
     torch.manual_seed(cfg.seed)
     model = build_model(cfg).to(dev)
     nparams = sum(p.numel() for p in model.parameters())
     g = torch.Generator(device="cpu").manual_seed(cfg.seed + rank)
-    tokens = torch.randint(0, cfg.vocab_size, (4_000_000,), generator=g).to(dev)
+    tokens = torch.randint(0, cfg.vocab_size, (4_000_000 if cuda else 100_000,), generator=g).to(dev)
     it = ShardedWindows(tokens, cfg.block_size, cfg.micro_batch_size, rank, world, cfg.seed)
     tr = Trainer(cfg, model, world, rank, dev)
     for _ in range(args.warmup):
         tr.step(it.next)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    sync()
     t0 = time.perf_counter()
+    loss = torch.zeros(())
     for _ in range(args.steps):
         loss = tr.step(it.next)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    sync()
     el = time.perf_counter() - t0
     if world > 1:
         t = torch.tensor([el], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    tok = world * cfg.micro_batch_size * cfg.block_size * args.steps
-    return {"metric": "train tokens/sec", "value": round(tok / el, 1), "unit": "tokens/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
-            "data": "synthetic", "final_loss": float(loss),
-            "config": {"workload": (f"cfg3: AlternatingDiffTransformer(12000,768,6,10,2048,n_terms={cfg.n_terms}) "
-                                    "training step" if arch == "ndiff" else
-                                    "cfg4: DiffTransformer(12000,1024,8,20,2048) DP training step"),
-                       "params": nparams, "micro_batch_per_gpu": cfg.micro_batch_size,
-                       "global_batch": cfg.micro_batch_size * world, "seq_len": cfg.block_size,
-                       "parallelism": f"dp{world} (bucketed RCCL all-reduce, {cfg.bucket_cap_mb} MB buckets)"}}
+    tok = world * cfg.micro_batch_size * cfg.block_size * max(args.steps, 1)
+    tps = tok / el if el > 0 else 0.0
+    fpt = model_flops_per_token(model, cfg)
+    workload = {"cpu-dry": "CPU/gloo dry run: StandardTransformer(256,64,4,2,32) training step",
+                "ndiff": f"cfg3: AlternatingDiffTransformer(12000,768,6,10,2048,n_terms={cfg.n_terms}) training step",
+                }.get(arch, "cfg4: DiffTransformer(12000,1024,8,20,2048) DP training step")
+    res = {"metric": "train tokens/sec", "value": round(tps, 1), "unit": "tokens/s", "n_gpus": world,
+           "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / max(args.steps, 1) * 1e3, 3),
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+           "dtype": "bf16" if cfg.dtype == "bf16" else cfg.dtype, "data": "synthetic", "final_loss": float(loss),
+           "config": {"workload": workload, "params": nparams, "micro_batch_per_gpu": cfg.micro_batch_size,
+                      "global_batch": cfg.micro_batch_size * world, "seq_len": cfg.block_size,
+                      "parallelism": f"dp{world} (bucketed {'RCCL' if cuda else 'gloo'} all-reduce, "
+                                     f"{cfg.bucket_cap_mb} MB buckets, overlapped with backward)"}}
+    if cuda:
+        res["model_tflops"] = round(fpt * tps / 1e12, 2)
+        res["mfu"] = round(fpt * tps / 1e12 / (world * PEAK_BF16_TFLOPS), 4)
+        res["flops_per_token"] = fpt
+    return res
 
 
 def main():

@@ -105,13 +105,25 @@ def apply_rotary_emb(x: Tensor, freqs_cis: Tensor) -> Tensor:
 
 
 # ------------------------------------------------------------ attention ---
+_TRIL: Dict[int, Tensor] = {}
+
+
+def _tril(T: int) -> Tensor:
+    """The reference's persistent fp32 ``tril`` buffer (diff_transformer.py:31),
+    built once per size like a registered buffer, not per call."""
+    t = _TRIL.get(T)
+    if t is None:
+        t = _TRIL[T] = torch.tril(torch.ones(T, T, dtype=torch.float32))
+    return t
+
+
 def causal_softmax(q: Tensor, k: Tensor, scale: float) -> Tensor:
-    """``softmax(masked_fill(q k^T * scale, tril==0, -inf))`` for (B,T,d) inputs
-    (diff_transformer.py:57-65)."""
+    """``softmax(masked_fill(q k^T * scale, tril[:T,:T]==0, -inf))`` for (B,T,d)
+    inputs (diff_transformer.py:57-65): the ``== 0`` compare runs every call, as in
+    the reference; the buffer itself is persistent."""
     T = q.shape[1]
     att = (q @ k.transpose(-2, -1)) * scale
-    keep = torch.tril(torch.ones(T, T, dtype=torch.float32))
-    att = att.masked_fill(keep == 0, float("-inf"))
+    att = att.masked_fill(_tril(T)[:T, :T] == 0, float("-inf"))
     return F.softmax(att, dim=-1)
 
 
