@@ -81,6 +81,16 @@ def test_module_bf16_autocast(golden, prefix):
         m, x, out = _run_module(case, g, torch.autocast("cuda", dtype=torch.bfloat16))
         assert rel_err(out.float(), g["out"]) < BF16_TOL, (case, "out")
         assert rel_err(x.grad, g["grad_in0"]) < BF16_TOL, (case, "grad_in0")
+        # every parameter gradient too: projections, GroupLayerNorm, and the lambda_q / lambda_k
+        # grads that reach the parameters through d(coef) (fp32 params, bf16 matmuls)
+        named = dict(m.named_parameters())
+        for k, ref in g.grads().items():
+            got = named[k].grad
+            assert got is not None, (case, k)
+            if float(np.abs(ref).max()) == 0.0:
+                assert float(got.abs().max()) < 1e-4, (case, k)
+            else:
+                assert rel_err(got, ref) < BF16_TOL, (case, k, rel_err(got, ref))
 
 
 @pytest.mark.parametrize("case,ctor", [
@@ -170,10 +180,11 @@ def test_trainer_steps_on_gpu(model, dtype):
 @pytest.mark.parametrize("hs,T", [(64, 97), (128, 160)])
 def test_control_mha_on_fused_kernel(dtype, hs, T):
     """control.py's MultiHeadAttention (control.py:64-78) on the GPU runs the fused
-    kernels' N=1, coef 1, dv=hs case; compared with the same module's PyTorch path
-    (the one pinned to the reference fixtures by test_control_cpu_matches_golden)
-    in fp64 on the CPU: output, input gradient and every weight gradient."""
+    kernels' N=1, coef 1, dv=hs case; compared in fp64 on the CPU with the oracle's
+    restatement (orc.control_multihead, pinned to the reference fixtures) and with the
+    same module's PyTorch path: output, input gradient and every weight gradient."""
     from differential_transformer_replication_amd import control as C
+    from oracle import diffattn_oracle as orc
     torch.manual_seed(3)
     H, C_ = 3, 3 * hs
     m = C.MultiHeadAttention(H, hs, C_, 0.0, 256)
@@ -184,6 +195,11 @@ def test_control_mha_on_fused_kernel(dtype, hs, T):
     out64 = ref(x64)
     (out64 * g.double()).sum().backward()
     grads64 = {n: p.grad.clone() for n, p in ref.named_parameters()}
+    sd = {k: (v.detach().clone().requires_grad_(True) if v.is_floating_point() else v)
+          for k, v in ref.state_dict().items()}
+    xo = x.double().requires_grad_(True)
+    out_orc = orc.control_multihead(xo, sd, H, 256)
+    (out_orc * g.double()).sum().backward()
     mg = C.MultiHeadAttention(H, hs, C_, 0.0, 256)
     mg.load_state_dict({k: v.float() if v.is_floating_point() else v for k, v in ref.state_dict().items()})
     mg = mg.to(DEV).to(dtype)
@@ -200,3 +216,8 @@ def test_control_mha_on_fused_kernel(dtype, hs, T):
     assert rel(xg.grad, x64.grad) < tol
     for n, p in mg.named_parameters():
         assert rel(p.grad, grads64[n]) < tol, n
+    # the oracle (reference algorithm restated)
+    assert rel(out, out_orc.detach()) < tol
+    assert rel(xg.grad, xo.grad) < tol
+    for n, p in mg.named_parameters():
+        assert rel(p.grad, sd[n].grad) < tol, ("oracle", n)

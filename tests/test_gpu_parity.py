@@ -182,3 +182,94 @@ def test_rope_kernel_matches_reference_fixture(golden):
     _lib.check(lib.dta_rope(a, _lib.stream_handle(src.device)))
     torch.cuda.synchronize()
     assert (dst.view(B, T, hs).cpu() - want).abs().max().item() < 1e-6
+
+
+# ---- full-length shapes, checked on sampled query rows ----------------------------------
+def _sample_rows(T, n, seed):
+    fixed = [0, 1, 31, 32, 63, 64, 127, 128, 255, 256, 511, 512, T // 2 - 1, T // 2, T - 65, T - 64, T - 2, T - 1]
+    g = torch.Generator().manual_seed(seed)
+    rnd = torch.randint(0, T, (n,), generator=g).tolist()
+    return sorted({r for r in fixed + rnd if 0 <= r < T})
+
+
+def _rows_reference(q, k, v, coef, rows, do_rows):
+    """fp64 restatement of diff_core (diff_transformer.py:57-72 / Ndiff_transformer.py:
+    102-125) for the query rows ``rows`` of ONE (b, h) over the full key range.
+    q, k: (T, N, hs); v: (T, dv); coef (N,); do_rows (R, dv).  Returns out_R and the
+    gradients of sum(out_R * do_R) w.r.t. q (rows only), k, v and coef -- equal to the
+    full problem's gradients when dO is zero on every other row."""
+    T, N, hs = k.shape
+    q = q.double().requires_grad_(True)
+    k = k.double().requires_grad_(True)
+    v = v.double().requires_grad_(True)
+    c = coef.double().requires_grad_(True)
+    r = torch.tensor(rows)
+    keep = torch.arange(T)[None, :] <= r[:, None]                       # causal: key <= query
+    out = 0
+    for i in range(N):
+        s = (q[r, i] @ k[:, i].t()) / math.sqrt(hs)
+        a = torch.softmax(s.masked_fill(~keep, float("-inf")), dim=-1)
+        out = out + c[i] * (a @ v)
+    (out * do_rows.double()).sum().backward()
+    return out.detach(), q.grad, k.grad, v.grad, c.grad
+
+
+def _long_case(B, H, N, hs, T, pairs, n_rows, dtype=torch.bfloat16, seed=0):
+    ops = _ops()
+    dv = 2 * hs
+    W = ops.packed_width(H, N, hs, dv)
+    nq = H * N * hs
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    qkv = torch.randn(B, T, W, device=DEV, generator=g).to(dtype)
+    coef = torch.randn(H, N, device=DEV, generator=g) * 0.5
+    coef[:, 0] = 1.0
+    do = torch.zeros(B, T, H, dv, device=DEV, dtype=dtype)
+    rows = {}
+    for j, (b, h) in enumerate(pairs):
+        rows[(b, h)] = _sample_rows(T, n_rows, seed + j)
+        r = torch.tensor(rows[(b, h)], device=DEV)
+        do[b, r, h] = torch.randn(len(r), dv, device=DEV, generator=g).to(dtype)
+    xg = qkv.clone().requires_grad_(True)
+    cg = coef.clone().requires_grad_(True)
+    out = ops.diff_attention(xg, cg, H, N, hs)
+    out.backward(do.view(B, T, H * dv))
+    torch.cuda.synchronize()
+    tol = TOL[dtype]
+    out = out.view(B, T, H, dv)
+    gx = xg.grad
+    for (b, h), rr in rows.items():
+        x = qkv[b].float().cpu()
+        q = x[:, :nq].view(T, H, N, hs)[:, h]
+        k = x[:, nq:2 * nq].view(T, H, N, hs)[:, h]
+        v = x[:, 2 * nq:].view(T, H, dv)[:, h]
+        d_r = do[b, rr, h].float().cpu()
+        o_ref, dq_ref, dk_ref, dv_ref, dc_ref = _rows_reference(q, k, v, coef[h].cpu(), rr, d_r)
+        where = f"b={b} h={h}"
+        assert rel_err(out[b, rr, h].float().cpu(), o_ref) < tol, "O " + where
+        gb = gx[b].float().cpu()
+        dq = gb[:, :nq].view(T, H, N, hs)[:, h]
+        assert rel_err(dq[rr], dq_ref[rr]) < tol, "dQ " + where
+        others = torch.ones(T, dtype=torch.bool)
+        others[rr] = False
+        assert dq[others].abs().max().item() == 0.0, "dQ nonzero on rows with dO = 0 " + where
+        assert rel_err(gb[:, nq:2 * nq].view(T, H, N, hs)[:, h], dk_ref) < tol, "dK " + where
+        assert rel_err(gb[:, 2 * nq:].view(T, H, dv)[:, h], dv_ref) < tol, "dV " + where
+        assert rel_err(cg.grad[h].cpu(), dc_ref) < tol, "dcoef " + where
+
+
+def test_cfg5_long_context_sampled_rows():
+    """BASELINE configs[4]: causal T=32768, hs=128 (dv=256), N=2, bf16 -- the hs=128
+    plan's long K/V ring and its LSE over 32k keys, against fp64 on 48+ rows per head."""
+    _long_case(B=1, H=2, N=2, hs=128, T=32768, pairs=[(0, 0), (0, 1)], n_rows=48)
+
+
+def test_cfg2_full_shape_sampled_rows():
+    """BASELINE configs[1] at its full shape (B=8, H=16, hs=64, T=4096, bf16), checked on
+    sampled rows of (b, h) pairs spread over the grid (first, last, middle)."""
+    pairs = [(0, 0), (7, 15), (3, 7), (5, 2), (1, 12), (6, 9)]
+    _long_case(B=8, H=16, N=2, hs=64, T=4096, pairs=pairs, n_rows=40, seed=11)
+
+
+def test_ndiff_long_sampled_rows():
+    """N=4 at T=8192 (hs=64): the N-term plan over a long ring."""
+    _long_case(B=1, H=2, N=4, hs=64, T=8192, pairs=[(0, 0), (0, 1)], n_rows=32, seed=5)

@@ -12,7 +12,8 @@ import sys
 from collections import defaultdict
 
 NAMES = {"attn_fwd_kernel": "attn_fwd", "attn_dq_kernel": "attn_bwd_dq", "attn_dkdv_kernel": "attn_bwd_dkdv",
-         "decode_split_kernel": "decode_split", "decode_combine_kernel": "decode_combine"}
+         "decode_split_kernel": "decode_split", "decode_combine_kernel": "decode_combine",
+         "ln_fwd_kernel": "ln_fwd", "ln_bwd_kernel": "ln_bwd", "rope_kernel": "rope"}
 
 
 def per_kernel(path, counter):
@@ -27,7 +28,7 @@ def per_kernel(path, counter):
     return {k: sum(v) / len(v) for k, v in vals.items()}
 
 
-def main(src, dst):
+def main(src, dst, shape=None):
     fetch = per_kernel(src + "/pmc_fetch", "FETCH_SIZE")
     write = per_kernel(src + "/pmc_write", "WRITE_SIZE")
     out = {"source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes, python3 bench.py "
@@ -35,6 +36,10 @@ def main(src, dst):
            "units": "bytes per launch; FETCH_SIZE and WRITE_SIZE are KiB; FETCH_SIZE doubled (gfx950: counts half "
                     "the bytes of 16B/lane streaming reads, MI355X_MICROARCH.md HBM section)",
            "kernels": {}}
+    if shape:
+        # the attention workload these launches ran at (bench.shape_key); ln_* / rope are at
+        # their fixed hbm_bench shapes (bench.py hbm_bench docstring)
+        out["shape"] = shape
     for k in NAMES.values():
         if k not in fetch or k not in write:
             continue
@@ -48,4 +53,4 @@ def main(src, dst):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(sys.argv[1], sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else None)
