@@ -14,6 +14,7 @@ import torch.nn as nn
 from torch.nn import functional as F
 
 from . import kv_cache, ops
+from .packing import ensure_packed, packed_linear
 from ._compat import (emit_tril_hooks, lambda_init_value, check_seq_len, check_dropout, fill_if_changed,
                       mha_out_scale)
 from .diff_transformer import GroupLayerNorm, SwiGLU
@@ -121,12 +122,18 @@ class MultiHeadAlternatingDiffAttention(nn.Module):
         self.head_size = head_size
         self.n_terms = n_terms
         self.block_size = block_size
+        self._pack = {}                            # the shared storage of the heads' projections
 
-    def packed_weight(self) -> torch.Tensor:
+    def packed_params(self):
+        """Every head's projection weights in the kernel's packed row order."""
         q = [m.weight for h in self.heads for m in h.queries]
         k = [m.weight for h in self.heads for m in h.keys]
         v = [h.value.weight for h in self.heads]
-        return torch.cat(q + k + v, dim=0)
+        return q + k + v
+
+    def packed_weight(self) -> torch.Tensor:
+        """The pack the per-head weights are views of (no copy)."""
+        return ensure_packed(self.packed_params(), self._pack)
 
     def coefficients(self, layer_idx) -> torch.Tensor:
         init = lambda_init_value(layer_idx, self.heads[0].lambda_init)
@@ -144,7 +151,7 @@ class MultiHeadAlternatingDiffAttention(nn.Module):
         for h in self.heads:
             check_dropout(h.dropout, self.training)
         coef = self.coefficients(layer_idx)
-        qkv = F.linear(x, self.packed_weight())
+        qkv = packed_linear(x, self.packed_params(), self._pack)
         freqs = rope_table(self.heads[0].freqs_cis, T, self.head_size)
         out = ops.diff_attention(qkv, coef, self.num_heads, self.n_terms, self.head_size, freqs)
         gn = self.group_norm

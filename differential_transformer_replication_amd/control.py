@@ -18,6 +18,7 @@ from torch.nn import functional as F
 
 from . import kv_cache, ops
 from ._compat import emit_tril_hooks, check_seq_len
+from .packing import ensure_packed, packed_linear
 from .Ndiff_transformer import precompute_freqs_cis, apply_rotary_emb, rope_table
 
 __all__ = ["precompute_freqs_cis", "apply_rotary_emb", "Head", "MultiHeadAttention", "SwiGLU", "Block",
@@ -85,19 +86,26 @@ class MultiHeadAttention(nn.Module):
         self.dropout = nn.Dropout(dropout)
         self.num_heads = num_heads
         self.head_size = head_size
+        self._pack = {}                            # the shared storage of the heads' projections
+
+    def packed_params(self):
+        return ([h.query.weight for h in self.heads] + [h.key.weight for h in self.heads]
+                + [h.value.weight for h in self.heads])
+
+    def packed_weight(self) -> torch.Tensor:
+        return ensure_packed(self.packed_params(), self._pack)
 
     def forward(self, x):
         B, T, _ = x.shape
         check_seq_len(T, self.heads[0].block_size)
         H, hs = self.num_heads, self.head_size
-        w = torch.cat([h.query.weight for h in self.heads] + [h.key.weight for h in self.heads]
-                      + [h.value.weight for h in self.heads], 0)
+        qkv = packed_linear(x, self.packed_params(), self._pack)
         fc = self.heads[0].freqs_cis
         p = self.heads[0].dropout.p if self.training else 0.0
         if _fused_ok(x, p, hs):
-            out = _fused_attention(F.linear(x, w), H, hs, fc)
+            out = _fused_attention(qkv, H, hs, fc)
         else:
-            q, k, v = F.linear(x, w).view(B, T, 3, H, hs).permute(2, 0, 3, 1, 4)
+            q, k, v = qkv.view(B, T, 3, H, hs).permute(2, 0, 3, 1, 4)
             q, k = _rope_fp32(q, fc), _rope_fp32(k, fc)
             out = F.scaled_dot_product_attention(q, k, v, is_causal=True, dropout_p=p, scale=1.0 / (hs ** 0.5))
             out = out.transpose(1, 2).reshape(B, T, H * hs)

@@ -39,8 +39,52 @@
 #ifndef DTA_DQ_AHEAD
 #define DTA_DQ_AHEAD 0
 #endif
+// forward: the two waves of a SIMD run half a tile apart (see attn_fwd_kernel)
+#ifndef DTA_FWD_PINGPONG
+#define DTA_FWD_PINGPONG 0
+#endif
+// forward: every branch's QK^T chain before the softmax VALU, one rescale decision per tile
+#ifndef DTA_FWD_QKFIRST
+#define DTA_FWD_QKFIRST 0
+#endif
+
+#ifndef DTA_STAMPS
+#define DTA_STAMPS 0
+#endif
 
 namespace dta {
+
+// In-kernel cycle stamps (diagnostic builds, -DDTA_STAMPS=1; cdna_hip_programming.md
+// 7 'In-kernel stamps'): per-wave sums of the cycles between named points of the
+// tile loop, written once per wave to FwdParams/BwdParams::stamps.  The stamp's own
+// lgkmcnt(0) serialises LDS reads, so a stamped build is read for its SHARES only.
+struct Stamps {
+  static constexpr int NSEG = 8;
+  unsigned long long t = 0, s[NSEG] = {};
+  __device__ __forceinline__ static unsigned long long now() {
+    unsigned long long v;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : : "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return v;
+  }
+  __device__ __forceinline__ void start() { if constexpr (DTA_STAMPS) t = now(); }
+  template <int J>
+  __device__ __forceinline__ void lap() {
+    if constexpr (DTA_STAMPS) {
+      const unsigned long long n = now();
+      s[J] += n - t;
+      t = n;
+    }
+  }
+  __device__ __forceinline__ void flush(unsigned long long* out, int wave_id, int lane) {
+    if constexpr (DTA_STAMPS) {
+      if (out && lane == 0)
+#pragma unroll
+        for (int j = 0; j < NSEG; ++j) out[(int64_t)wave_id * NSEG + j] = s[j];
+    }
+  }
+};
 
 // ------------------------------------------------------------ LDS images ---
 template <int ROWB>
@@ -89,6 +133,19 @@ struct Img {
     }
   }
 };
+
+// Gradient through RoPE (Ndiff_transformer.py:11-22 backward), fused into the dQ / dK
+// epilogues: the kernels differentiate w.r.t. the ROTATED Q_i / K_i, and the
+// parameters' gradient is the conjugate rotation of that.  Registers 4g..4g+3 of a
+// lane hold columns e..e+3 (e % 4 == 0) of one row: two interleaved pairs, whose
+// [cos, sin] entries are 4 consecutive floats of the fp32 [T][hs/2][2] table.
+__device__ __forceinline__ void rope_inv4(const float* rope, int64_t row, int hs, int e, float& a0, float& a1,
+                                          float& a2, float& a3) {
+  const f32x4 t = *reinterpret_cast<const f32x4*>(rope + (row * (hs >> 1) + (e >> 1)) * 2);
+  const float b0 = fmaf(a0, t[0], a1 * t[1]), b1 = fmaf(a1, t[0], -a0 * t[1]);
+  const float b2 = fmaf(a2, t[2], a3 * t[3]), b3 = fmaf(a3, t[2], -a2 * t[3]);
+  a0 = b0; a1 = b1; a2 = b2; a3 = b3;
+}
 
 // ---- compile-time loops (asm immediates must be constants, not unrolled loop indices)
 template <class F, int... I>
@@ -444,10 +501,26 @@ __global__ __launch_bounds__(NW * 64, (FwdCfg<E, HS, N, DVC, NW, QREG>::WPE)) vo
   };
   const int tile_pieces = SRD ? KR::pieces(wave)
                               : N * stage_pieces<E, HS, BN, HS, NW>(wave) + stage_pieces<E, DVC, BN, DVC, NW>(wave);
-  for (int j = 0; j < NS - 1; ++j)
-    if (j < ntiles) stage_kv(j, j);
-  wait_vm(tile_pieces * max(0, min(NS - 1, ntiles) - 1));   // tile 0 (and the Q block) landed
-  lds_barrier();
+  // Ping-pong (PP): the two waves sharing a SIMD (w and w+4) run half a tile apart --
+  // one in its QK^T + softmax phase (A) while the other is in its PV phase (B) -- so
+  // the VALU-heavy half of one overlaps the MFMA-only half of the other instead of
+  // both hitting the VALU at once (MI355X_MICROARCH.md, two waves per SIMD).  The
+  // second half (G1) passes one extra barrier before the loop, the first half (G0)
+  // one after it.  Ring protocol (NS = 3 stages, checked in DESIGN.md): G0 stages
+  // tile t+1 at the start of its A(t) and waits for it at the end of its B(t); G1
+  // stages tile t+2 at the start of its B(t) and waits for tile t+1 at the end of
+  // its A(t).  Every buffer is refilled only after both halves finished its tile.
+  constexpr bool PP = DTA_FWD_PINGPONG && NW == 8 && SRD && sizeof(E) == 2 && CF::NS == 3;
+  const bool g1 = PP && wave >= NW / 2;
+  if constexpr (PP) {
+    if (ntiles > 0) stage_kv(0, 0);
+    if (g1 && ntiles > 1) stage_kv(1, 1);
+    wait_vm(g1 && ntiles > 1 ? tile_pieces : 0);               // tile 0 (and the Q block) landed
+  } else {
+    for (int j = 0; j < NS - 1; ++j)
+      if (j < ntiles) stage_kv(j, j);
+    wait_vm(tile_pieces * max(0, min(NS - 1, ntiles) - 1));   // tile 0 (and the Q block) landed
+  }  lds_barrier();
 
   f32x16 acc[N][NDB];
   float m[N], l[N];
@@ -462,164 +535,238 @@ __global__ __launch_bounds__(NW * 64, (FwdCfg<E, HS, N, DVC, NW, QREG>::WPE)) vo
   // static priority for the second-dispatched half (MI355X_MICROARCH.md, two waves per SIMD, item 4)
   if (NW == 8 && p.prio && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
 
+  // key = k0 + kb*32 + rowof(r); masked when key > qrow or key >= T
+  auto mask_scores = [&](int k0, f32x16 (&sa)[NKB]) {
+    const int lim = min(qrow, T - 1) - k0 - 4 * hf;
+#pragma unroll
+    for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sa[kb][r] = (kb * 32 + (r & 3) + 8 * (r >> 2) > lim) ? -INFINITY : sa[kb][r];
+  };
+  // this lane's row maximum: two independent v_max3 chains
+  auto row_max = [&](const f32x16 (&sa)[NKB]) -> float {
+    float a = -INFINITY, b = -INFINITY;
+#pragma unroll
+    for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; r += 4) {
+        a = fmaxf(fmaxf(a, sa[kb][r]), sa[kb][r + 1]);
+        b = fmaxf(fmaxf(b, sa[kb][r + 2]), sa[kb][r + 3]);
+      }
+    return fmaxf(a, b);
+  };
+  // P = exp2(S * scale*log2e - m), row sums (two chains), packed to the PV operand
+  auto exp_pack = [&](int i, f32x16 (&sa)[NKB], frag (&pf)[NKB * SPB]) {
+    const float mi = m[i];
+    float ls0 = 0.f, ls1 = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) {
+        const float e0 = exp2_fast(fmaf(sa[kb][r], p.sl2, -mi));
+        const float e1 = exp2_fast(fmaf(sa[kb][r + 1], p.sl2, -mi));
+        sa[kb][r] = e0;
+        sa[kb][r + 1] = e1;
+        ls0 += e0;
+        ls1 += e1;
+      }
+    l[i] += ls0 + ls1;
+#pragma unroll
+    for (int kb = 0; kb < NKB; ++kb) {
+      if constexpr (SPB == 2) {
+        pf[kb * 2 + 0] = O::template pack<0>(sa[kb]);
+        pf[kb * 2 + 1] = O::template pack<1>(sa[kb]);
+      } else {
+#pragma unroll
+        for (int s = 0; s < 16; ++s) pf[kb * SPB + s] = sa[kb][s];
+      }
+    }
+  };
+  // one branch's mask, max, deferred rescale (only when some row's max grew by > 2^THR), exp
+  auto softmax_branch = [&](int i, int k0, auto MASKED, f32x16 (&sa)[NKB], frag (&pf)[NKB * SPB]) {
+    if constexpr (decltype(MASKED)::value) mask_scores(k0, sa);
+    const float mx = wave_max_halves(row_max(sa)) * p.sl2;
+    if (__any(mx > m[i] + THR)) {
+      const float mnew = fmaxf(m[i], mx);
+      const float alpha = exp2_fast(m[i] - mnew);
+      m[i] = mnew;
+      l[i] *= alpha;
+#pragma unroll
+      for (int d = 0; d < NDB; ++d) acc[i][d] *= alpha;
+    }
+    exp_pack(i, sa, pf);
+  };
+  // QK^T + online softmax of one key tile for every branch, P packed as the PV B operand
+  auto phase_a = [&](int kt, auto MASKED, frag (&pf)[N][NKB * SPB]) {
+    constexpr bool MASK = decltype(MASKED)::value;
+    const int buf = kt % NS;
+    const int k0 = kt * BN;
+    const E* Kc = Kb + buf * N * BN * HS;
+    f32x16 sa[N][NKB];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const E* Ki = Kc + i * BN * HS;
+      if constexpr (sizeof(E) == 2) {
+        // row operands: byte R*ROWB + (Lrow ^ 32 s) for a 32-row block at row R
+        const int Lr = row_lane<KI::ROWB>(lane);
+        const char* kbase = reinterpret_cast<const char*>(Ki);
+        const char* qbase = reinterpret_cast<const char*>(Qs + i * BM * HS) + wave * 32 * QI::ROWB;
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb) sa[i][kb] = f32x16{};
+        if constexpr (NSQ * (NKB + 1) <= 12) {
+          // every operand read of this branch's S^T issued ahead of its MFMA chain,
+          // so the chain waits on the LDS latency once instead of per k-step
+          // (head sizes <= 64; at 128 the 24 fragments do not fit the registers)
+          frag kfr[NKB][NSQ], qfr[NSQ];
+#pragma unroll
+          for (int s = 0; s < NSQ; ++s) {
+            const int o = Lr ^ (32 * s);
+            if constexpr (QREG) qfr[s] = qf[i][s];
+            else qfr[s] = *reinterpret_cast<const frag*>(qbase + o);
+#pragma unroll
+            for (int kb = 0; kb < NKB; ++kb) kfr[kb][s] = *reinterpret_cast<const frag*>(kbase + kb * 32 * KI::ROWB + o);
+          }
+#pragma unroll
+          for (int s = 0; s < NSQ; ++s)
+#pragma unroll
+            for (int kb = 0; kb < NKB; ++kb) sa[i][kb] = O::mma(kfr[kb][s], qfr[s], sa[i][kb]);
+          __builtin_amdgcn_sched_group_barrier(0x100, NSQ * (NKB + (QREG ? 0 : 1)), 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, NSQ * NKB, 0);
+        } else {
+#pragma unroll
+          for (int s = 0; s < NSQ; ++s) {
+            const int o = Lr ^ (32 * s);
+            frag qb;
+            if constexpr (QREG) qb = qf[i][s];
+            else qb = *reinterpret_cast<const frag*>(qbase + o);
+#pragma unroll
+            for (int kb = 0; kb < NKB; ++kb)
+              sa[i][kb] = O::mma(*reinterpret_cast<const frag*>(kbase + kb * 32 * KI::ROWB + o), qb, sa[i][kb]);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb) {
+          sa[i][kb] = f32x16{};
+#pragma unroll
+          for (int s = 0; s < NSQ; ++s) {
+            frag qb;
+            if constexpr (QREG) qb = qf[i][s];
+            else qb = QI::row(Qs + i * BM * HS, wave * 32 + c32, s, hf);
+            sa[i][kb] = O::mma(KI::row(Ki, kb * 32 + c32, s, hf), qb, sa[i][kb]);
+          }
+        }
+      }
+      if constexpr (!DTA_FWD_QKFIRST) softmax_branch(i, k0, MASKED, sa[i], pf[i]);
+    }
+    if constexpr (DTA_FWD_QKFIRST) {
+      // every branch's S^T first (above), then the maxima and ONE rescale decision for all
+      // branches, so the VALU of branch 0 can run beside branch 1's MFMA chain
+      float mx[N];
+      bool grow = false;
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        if constexpr (MASK) mask_scores(k0, sa[i]);
+        mx[i] = wave_max_halves(row_max(sa[i])) * p.sl2;
+        grow = grow || mx[i] > m[i] + THR;
+      }
+      if (__any(grow)) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+          const float mnew = fmaxf(m[i], mx[i]);
+          const float alpha = exp2_fast(m[i] - mnew);
+          m[i] = mnew;
+          l[i] *= alpha;
+#pragma unroll
+          for (int d = 0; d < NDB; ++d) acc[i][d] *= alpha;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < N; ++i) exp_pack(i, sa[i], pf[i]);
+    }
+  };
+  // O_i^T += V^T P_i^T, one V fragment feeds every branch
+  auto phase_b = [&](int kt, const frag (&pf)[N][NKB * SPB]) {
+    const E* Vc = Vb + (kt % NS) * BN * DVC;
+    if constexpr (sizeof(E) == 2) {
+      const unsigned vb = lds_addr(Vc);
+      const int Lv = tr_lane<VI::ROWB>(lane);
+      sfor<NDB>([&](auto D) {
+        constexpr int d = decltype(D)::value;
+        lds64 r[NKB][4];
+        const unsigned a0 = vb + (Lv ^ (64 * d)), a1 = vb + (Lv ^ (64 * d + 32));
+        sfor<NKB>([&](auto KB) { tr_issue<VI::ROWB, 32 * decltype(KB)::value>(r[decltype(KB)::value], a0, a1); });
+        lgkm_pin<NKB>(r);
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            const frag va = tr_frag<E>(r[kb], s);
+#pragma unroll
+            for (int i = 0; i < N; ++i) acc[i][d] = O::mma(va, pf[i][kb * 2 + s], acc[i][d]);
+          }
+      });
+    } else {
+#pragma unroll
+      for (int d = 0; d < NDB; ++d)
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+          for (int s = 0; s < SPB; ++s) {
+            const frag va = VI::tr_perm(Vc, kb * 32, s, hf, d * 32, lane);
+#pragma unroll
+            for (int i = 0; i < N; ++i) acc[i][d] = O::mma(va, pf[i][kb * SPB + s], acc[i][d]);
+          }
+    }
+  };
+
   // two loops over straight-line bodies: tiles strictly below the block's first
   // query row and inside T need no mask; the block's diagonal / tail tiles do
   // (one loop body with both variants behind a branch spills)
+  Stamps st;
   auto step = [&](int kt, auto MASKED) {
-    constexpr bool MASK = decltype(MASKED)::value;
     // keep lane-derived addresses loop-variant: recomputed per tile instead of
     // hoisted into (spilled) registers across the whole loop
     asm volatile("" : "+v"(lane));
     tid = (wave << 6) + lane; hf = lane >> 5; c32 = lane & 31;
     qrow = qw0 + c32;
-    const int buf = kt % NS;
-    if (kt + NS - 1 < ntiles) stage_kv(kt + NS - 1, (kt + NS - 1) % NS);
-    const int k0 = kt * BN;
-    if (wave_live && k0 <= qw0 + 31) {
-      const E* Kc = Kb + buf * N * BN * HS;
-      const E* Vc = Vb + buf * BN * DVC;
-      {
+    const bool live = wave_live && kt * BN <= qw0 + 31;
+    st.lap<7>();
+    if constexpr (PP) {
+      if (!g1 && kt + 1 < ntiles) stage_kv(kt + 1, (kt + 1) % NS);
+      frag pf[N][NKB * SPB];
+      if (live) phase_a(kt, MASKED, pf);
+      if (g1) wait_vm(0);                    // tile kt+1 (staged at B(kt-1)) before G0 reads it
+      lds_barrier();
+      if (g1 && kt + 2 < ntiles) stage_kv(kt + 2, (kt + 2) % NS);
+      if (live) phase_b(kt, pf);
+      if (!g1) wait_vm(0);                   // tile kt+1 (staged at A(kt))
+      lds_barrier();
+    } else {
+      if (kt + NS - 1 < ntiles) stage_kv(kt + NS - 1, (kt + NS - 1) % NS);
+      st.lap<0>();
+      if (live) {
         frag pf[N][NKB * SPB];
-#pragma unroll
-        for (int i = 0; i < N; ++i) {
-          f32x16 sa[NKB];
-          const E* Ki = Kc + i * BN * HS;
-          if constexpr (sizeof(E) == 2) {
-            // row operands: byte R*ROWB + (Lrow ^ 32 s) for a 32-row block at row R
-            const int Lr = row_lane<KI::ROWB>(lane);
-            const char* kbase = reinterpret_cast<const char*>(Ki);
-            const char* qbase = reinterpret_cast<const char*>(Qs + i * BM * HS) + wave * 32 * QI::ROWB;
-#pragma unroll
-            for (int kb = 0; kb < NKB; ++kb) sa[kb] = f32x16{};
-            if constexpr (NSQ * (NKB + 1) <= 12) {
-              // every operand read of this branch's S^T issued ahead of its MFMA chain,
-              // so the chain waits on the LDS latency once instead of per k-step
-              // (head sizes <= 64; at 128 the 24 fragments do not fit the registers)
-              frag kfr[NKB][NSQ], qfr[NSQ];
-#pragma unroll
-              for (int s = 0; s < NSQ; ++s) {
-                const int o = Lr ^ (32 * s);
-                if constexpr (QREG) qfr[s] = qf[i][s];
-                else qfr[s] = *reinterpret_cast<const frag*>(qbase + o);
-#pragma unroll
-                for (int kb = 0; kb < NKB; ++kb) kfr[kb][s] = *reinterpret_cast<const frag*>(kbase + kb * 32 * KI::ROWB + o);
-              }
-#pragma unroll
-              for (int s = 0; s < NSQ; ++s)
-#pragma unroll
-                for (int kb = 0; kb < NKB; ++kb) sa[kb] = O::mma(kfr[kb][s], qfr[s], sa[kb]);
-              __builtin_amdgcn_sched_group_barrier(0x100, NSQ * (NKB + (QREG ? 0 : 1)), 0);
-              __builtin_amdgcn_sched_group_barrier(0x008, NSQ * NKB, 0);
-            } else {
-#pragma unroll
-              for (int s = 0; s < NSQ; ++s) {
-                const int o = Lr ^ (32 * s);
-                frag qb;
-                if constexpr (QREG) qb = qf[i][s];
-                else qb = *reinterpret_cast<const frag*>(qbase + o);
-#pragma unroll
-                for (int kb = 0; kb < NKB; ++kb)
-                  sa[kb] = O::mma(*reinterpret_cast<const frag*>(kbase + kb * 32 * KI::ROWB + o), qb, sa[kb]);
-              }
-            }
-          } else {
-#pragma unroll
-            for (int kb = 0; kb < NKB; ++kb) {
-              sa[kb] = f32x16{};
-#pragma unroll
-              for (int s = 0; s < NSQ; ++s) {
-                frag qb;
-                if constexpr (QREG) qb = qf[i][s];
-                else qb = QI::row(Qs + i * BM * HS, wave * 32 + c32, s, hf);
-                sa[kb] = O::mma(KI::row(Ki, kb * 32 + c32, s, hf), qb, sa[kb]);
-              }
-            }
-          }
-          if constexpr (MASK) {
-            // key = k0 + kb*32 + rowof(r); masked when key > qrow or key >= T
-            const int lim = min(qrow, T - 1) - k0 - 4 * hf;
-#pragma unroll
-            for (int kb = 0; kb < NKB; ++kb)
-#pragma unroll
-              for (int r = 0; r < 16; ++r)
-                sa[kb][r] = (kb * 32 + (r & 3) + 8 * (r >> 2) > lim) ? -INFINITY : sa[kb][r];
-          }
-          float mx = -INFINITY;
-#pragma unroll
-          for (int kb = 0; kb < NKB; ++kb)
-#pragma unroll
-            for (int r = 0; r < 16; r += 2) mx = fmaxf(mx, fmaxf(sa[kb][r], sa[kb][r + 1]));
-          mx = wave_max_halves(mx) * p.sl2;
-          if (__any(mx > m[i] + THR)) {          // rescale only when some row's max grew by > 2^THR
-            const float mnew = fmaxf(m[i], mx);
-            const float alpha = exp2_fast(m[i] - mnew);
-            m[i] = mnew;
-            l[i] *= alpha;
-#pragma unroll
-            for (int d = 0; d < NDB; ++d) acc[i][d] *= alpha;
-          }
-          const float mi = m[i];
-          float ls = 0.f;
-#pragma unroll
-          for (int kb = 0; kb < NKB; ++kb)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              const float e = exp2_fast(fmaf(sa[kb][r], p.sl2, -mi));
-              sa[kb][r] = e;
-              ls += e;
-            }
-          l[i] += ls;
-#pragma unroll
-          for (int kb = 0; kb < NKB; ++kb) {
-            if constexpr (SPB == 2) {
-              pf[i][kb * 2 + 0] = O::template pack<0>(sa[kb]);
-              pf[i][kb * 2 + 1] = O::template pack<1>(sa[kb]);
-            } else {
-#pragma unroll
-              for (int s = 0; s < 16; ++s) pf[i][kb * SPB + s] = sa[kb][s];
-            }
-          }
-        }
-        // O_i^T += V^T P_i^T, one V fragment feeds every branch
-        if constexpr (sizeof(E) == 2) {
-          const unsigned vb = lds_addr(Vc);
-          const int Lv = tr_lane<VI::ROWB>(lane);
-          sfor<NDB>([&](auto D) {
-            constexpr int d = decltype(D)::value;
-            lds64 r[NKB][4];
-            const unsigned a0 = vb + (Lv ^ (64 * d)), a1 = vb + (Lv ^ (64 * d + 32));
-            sfor<NKB>([&](auto KB) { tr_issue<VI::ROWB, 32 * decltype(KB)::value>(r[decltype(KB)::value], a0, a1); });
-            lgkm_pin<NKB>(r);
-#pragma unroll
-            for (int kb = 0; kb < NKB; ++kb)
-#pragma unroll
-              for (int s = 0; s < 2; ++s) {
-                const frag va = tr_frag<E>(r[kb], s);
-#pragma unroll
-                for (int i = 0; i < N; ++i) acc[i][d] = O::mma(va, pf[i][kb * 2 + s], acc[i][d]);
-              }
-          });
-        } else {
-#pragma unroll
-          for (int d = 0; d < NDB; ++d)
-#pragma unroll
-            for (int kb = 0; kb < NKB; ++kb)
-#pragma unroll
-              for (int s = 0; s < SPB; ++s) {
-                const frag va = VI::tr_perm(Vc, kb * 32, s, hf, d * 32, lane);
-#pragma unroll
-                for (int i = 0; i < N; ++i) acc[i][d] = O::mma(va, pf[i][kb * SPB + s], acc[i][d]);
-              }
-        }
+        phase_a(kt, MASKED, pf);
+        st.lap<1>();
+        phase_b(kt, pf);
+        st.lap<2>();
       }
+      // tile kt+1 must have landed; younger tiles may stay in flight
+      wait_vm(tile_pieces * max(0, min(NS - 2, ntiles - 2 - kt)));
+      st.lap<3>();
+      lds_barrier();
+      st.lap<4>();
     }
-    // tile kt+1 must have landed; younger tiles may stay in flight
-    wait_vm(tile_pieces * max(0, min(NS - 2, ntiles - 2 - kt)));
-    lds_barrier();
   };
+  st.start();
+  if (g1) lds_barrier();                     // PP: the second half starts one phase behind
   const int nfull = min(ntiles, min((q0 + 1) / BN, T / BN));
   for (int kt = 0; kt < nfull; ++kt) step(kt, std::false_type{});
   for (int kt = nfull; kt < ntiles; ++kt) step(kt, std::true_type{});
+  if (PP && !g1) lds_barrier();              // ... and the first half ends one phase later
+  st.lap<5>();
+  st.flush(p.stamps, lin * NW + wave, lane);
 
   if (!wave_live || qrow >= T) return;
   float inv[N];
@@ -935,8 +1082,9 @@ void attn_dq_kernel(BwdParams p) {
       for (int g = 0; g < 4; ++g) {
         const int e = d * 32 + 8 * g + 4 * hf;
         if (e >= HS) continue;
-        const float a0 = dq[i][d][4 * g] * p.scale, a1 = dq[i][d][4 * g + 1] * p.scale;
-        const float a2 = dq[i][d][4 * g + 2] * p.scale, a3 = dq[i][d][4 * g + 3] * p.scale;
+        float a0 = dq[i][d][4 * g] * p.scale, a1 = dq[i][d][4 * g + 1] * p.scale;
+        float a2 = dq[i][d][4 * g + 2] * p.scale, a3 = dq[i][d][4 * g + 3] * p.scale;
+        if (p.rope) rope_inv4(p.rope, qrow, HS, e, a0, a1, a2, a3);
         if constexpr (OUTF32) {
           store4<float>(p.dq32 + ((((int64_t)b * T + qrow) * p.H + hh) * N + i) * HS + e, a0, a1, a2, a3);
         } else {
@@ -1154,6 +1302,7 @@ __global__ __launch_bounds__(NW * 64, (NW >= 8 ? 2 : 1)) void attn_dkdv_kernel(B
   // masked diagonal tiles, unmasked interior, masked ragged tail tile; each loop
   // is one straight-line body (both variants behind a branch spill).  Lanes with
   // key >= T only pollute their own (never stored) dK/dV columns.
+  Stamps st;
   auto step = [&](int t, auto MASKED) {
     constexpr bool MASK = decltype(MASKED)::value;
     // keep lane-derived addresses loop-variant: recomputed per tile instead of
@@ -1164,6 +1313,7 @@ __global__ __launch_bounds__(NW * 64, (NW >= 8 ? 2 : 1)) void attn_dkdv_kernel(B
     const int buf = t % NS;
     const int q0 = kb0 + t * BQ;
     if (t + NS - 1 < ntiles) stage_q(q0 + (NS - 1) * BQ, (t + NS - 1) % NS);
+    st.lap<0>();
     if (wave_keys && q0 + BQ - 1 >= kw0) {
       const char* sg = ringb + buf * RG::SB;
       const E* Qc = SRD ? reinterpret_cast<const E*>(sg) : Qb + buf * N * BQ * HSP;
@@ -1183,6 +1333,7 @@ __global__ __launch_bounds__(NW * 64, (NW >= 8 ? 2 : 1)) void attn_dkdv_kernel(B
           for (int s = 0; s < NSV; ++s) dpa = O::mma(DI::row(Dc, c32, s, hf), vf[s], dpa);
         }
       }
+      st.lap<1>();
       f32x16 pc = f32x16{};
       // rows q0 + rowof(r) > lim are masked: query < key, or past the end
       const int lim_lo = krow - q0 - 4 * hf;          // masked if rowof_c < lim_lo (query < key)
@@ -1255,6 +1406,7 @@ __global__ __launch_bounds__(NW * 64, (NW >= 8 ? 2 : 1)) void attn_dkdv_kernel(B
           }
         }
       }
+      st.lap<2>();
       if constexpr (DVV) {
         if constexpr (sizeof(E) == 2) {
           const unsigned db = lds_addr(Dc);
@@ -1284,14 +1436,19 @@ __global__ __launch_bounds__(NW * 64, (NW >= 8 ? 2 : 1)) void attn_dkdv_kernel(B
       }
       }
     }
+    st.lap<3>();
     wait_vm(tile_pieces * max(0, min(NS - 2, ntiles - 2 - t)));
+    st.lap<4>();
     lds_barrier();
+    st.lap<5>();
   };
+  st.start();
   const int thead = min(ntiles, (BK - 2) / BQ + 1);                  // q0 < kb0 + BK - 1
   const int ttail = max(thead, ntiles - ((T - kb0) % BQ != 0 ? 1 : 0));  // q0 + BQ > T
   for (int t = 0; t < thead; ++t) step(t, std::true_type{});
   for (int t = thead; t < ttail; ++t) step(t, std::false_type{});
   for (int t = ttail; t < ntiles; ++t) step(t, std::true_type{});
+  st.flush(p.stamps, lin * NW + wave, lane);
 
   if (!wave_keys || krow >= T) return;
   if constexpr (DK) {
@@ -1303,9 +1460,12 @@ __global__ __launch_bounds__(NW * 64, (NW >= 8 ? 2 : 1)) void attn_dkdv_kernel(B
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int e = d * 32 + 8 * g + 4 * hf;
-          if (e < HS)
-            store4<E>(gdk + i * p.dk.si + e, dk[i][d][4 * g] * p.scale, dk[i][d][4 * g + 1] * p.scale,
-                      dk[i][d][4 * g + 2] * p.scale, dk[i][d][4 * g + 3] * p.scale);
+          if (e < HS) {
+            float a0 = dk[i][d][4 * g] * p.scale, a1 = dk[i][d][4 * g + 1] * p.scale;
+            float a2 = dk[i][d][4 * g + 2] * p.scale, a3 = dk[i][d][4 * g + 3] * p.scale;
+            if (p.rope) rope_inv4(p.rope, krow, HS, e, a0, a1, a2, a3);
+            store4<E>(gdk + i * p.dk.si + e, a0, a1, a2, a3);
+          }
         }
   }
   if constexpr (DVV) {
@@ -1568,8 +1728,10 @@ __global__ __launch_bounds__(256, 1) void attn_dkdv4_kernel(BwdParams p) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int e = d * 32 + 8 * g + 4 * hf;
-        store4<E>(gdk + i * p.dk.si + e, dk[i][d][4 * g] * p.scale, dk[i][d][4 * g + 1] * p.scale,
-                  dk[i][d][4 * g + 2] * p.scale, dk[i][d][4 * g + 3] * p.scale);
+        float a0 = dk[i][d][4 * g] * p.scale, a1 = dk[i][d][4 * g + 1] * p.scale;
+        float a2 = dk[i][d][4 * g + 2] * p.scale, a3 = dk[i][d][4 * g + 3] * p.scale;
+        if (p.rope) rope_inv4(p.rope, krow, HS, e, a0, a1, a2, a3);
+        store4<E>(gdk + i * p.dk.si + e, a0, a1, a2, a3);
       }
   E* gdv = reinterpret_cast<E*>(p.dv.p) + b * p.dv.sb + (int64_t)krow * p.dv.st + hh * p.dv.sh;
 #pragma unroll

@@ -100,7 +100,32 @@ static int wave_prio() {
   return v;
 }
 
+#ifndef DTA_STAMPS
+#define DTA_STAMPS 0
+#endif
+#if DTA_STAMPS
+// diagnostic builds only: one device buffer for the kernels' per-wave stamp sums
+static unsigned long long* stamp_buf() {
+  static unsigned long long* b = [] {
+    void* p = nullptr;
+    if (hipMalloc(&p, 64 << 20) || hipMemset(p, 0, 64 << 20)) p = nullptr;
+    return (unsigned long long*)p;
+  }();
+  return b;
+}
+#else
+static unsigned long long* stamp_buf() { return nullptr; }
+#endif
+
 extern "C" {
+
+#if DTA_STAMPS
+// copy the stamp buffer to the host (diagnostic builds only; not in include/diffattn.h)
+int dta_debug_stamps(void* dst, size_t bytes) {
+  if (!stamp_buf() || bytes > (64u << 20)) return DTA_ERR_INVALID;
+  return hipMemcpy(dst, stamp_buf(), bytes, hipMemcpyDeviceToHost) ? DTA_ERR_LAUNCH : DTA_OK;
+}
+#endif
 
 int dta_abi_version(void) { return DTA_ABI_VERSION; }
 
@@ -134,6 +159,7 @@ int dta_attn_fwd(const dta_attn_fwd_args* a, void* stream) {
   p.B = a->B; p.T = a->T; p.H = a->H; p.N = a->n_terms; p.HS = a->head_size; p.DV = a->dv;
   p.sl2 = a->scale * kLog2e;
   p.prio = wave_prio();
+  p.stamps = stamp_buf();
   return status(launch_attn_fwd(a->dtype, p, (hipStream_t)stream));
 }
 
@@ -166,9 +192,12 @@ int dta_attn_bwd(const dta_attn_bwd_args* a, void* stream) {
   p.dq = t5(a->dq); p.dk = t5(a->dk); p.dv = t5(a->dv_out);
   p.lse = a->lse; p.delta = a->delta; p.coef = a->coef; p.dcoef = a->dcoef;
   p.dq32 = a->dq.ptr ? nullptr : a->dq_f32;
+  if (a->rope_freqs && (a->head_size % 4 || reinterpret_cast<uintptr_t>(a->rope_freqs) % 16)) return DTA_ERR_INVALID;
+  p.rope = a->rope_freqs;
   p.B = a->B; p.T = a->T; p.H = a->H; p.N = a->n_terms; p.HS = a->head_size; p.DV = a->dv;
   p.scale = a->scale; p.sl2 = a->scale * kLog2e;
   p.prio = wave_prio();
+  p.stamps = stamp_buf();
   int e = 0;
   if ((stages & DTA_BWD_DQ) && (e = launch_attn_dq(a->dtype, p, st))) return status(e);
   if ((stages & DTA_BWD_DKDV) && (e = launch_attn_dkdv(a->dtype, p, st))) return status(e);

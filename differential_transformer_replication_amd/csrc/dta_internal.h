@@ -18,6 +18,7 @@ struct FwdParams {
   int B, T, H, N, HS, DV;
   float sl2;           // scale * log2(e)
   int prio;            // 1: waves 4-7 of an 8-wave workgroup run at s_setprio 1
+  unsigned long long* stamps;   // diagnostic builds (DTA_STAMPS) only: per-wave segment cycle sums
 };
 
 struct BwdParams {
@@ -27,9 +28,11 @@ struct BwdParams {
   const float* coef;
   float* dcoef;        // accumulated by attn_dq (zeroed first)
   float* dq32;         // if set: dQ written as fp32 [b][t][h][i][d] instead of into dq
+  const float* rope;   // if set: fp32 [T][HS/2][2] table; dQ / dK leave through the inverse rotation
   int B, T, H, N, HS, DV;
   float sl2, scale;
   int prio;            // as FwdParams::prio
+  unsigned long long* stamps;   // as FwdParams::stamps
 };
 
 // per-dtype launchers (dtype index: 0 bf16, 1 f16, 2 f32); return hipError_t

@@ -16,6 +16,7 @@ import torch.nn as nn
 from torch.nn import functional as F
 
 from . import kv_cache, ops
+from .packing import ensure_packed, packed_linear
 from ._compat import (emit_tril_hooks, lambda_init_value, check_seq_len, check_dropout, fill_if_changed,
                       mha_out_scale)
 
@@ -104,13 +105,19 @@ class MultiHeadDiffAttention(nn.Module):
         self.num_heads = num_heads
         self.head_size = head_size
         self.block_size = block_size
+        self._pack = {}                            # the shared storage of the heads' projections
 
-    def packed_weight(self) -> torch.Tensor:
+    def packed_params(self):
+        """Every head's projection weights in the kernel's packed row order."""
         hs = self.heads
         q = [w for h in hs for w in (h.query1.weight, h.query2.weight)]
         k = [w for h in hs for w in (h.key1.weight, h.key2.weight)]
         v = [h.value.weight for h in hs]
-        return torch.cat(q + k + v, dim=0)
+        return q + k + v
+
+    def packed_weight(self) -> torch.Tensor:
+        """(2*H*2*hs + H*2hs, C): the pack the per-head weights are views of (no copy)."""
+        return ensure_packed(self.packed_params(), self._pack)
 
     def coefficients(self, layer_idx) -> torch.Tensor:
         init = lambda_init_value(layer_idx, self.heads[0].lambda_init)
@@ -124,7 +131,7 @@ class MultiHeadDiffAttention(nn.Module):
         for h in self.heads:
             check_dropout(h.dropout, self.training)
         coef = self.coefficients(layer_idx)
-        qkv = F.linear(x, self.packed_weight())
+        qkv = packed_linear(x, self.packed_params(), self._pack)
         out = ops.diff_attention(qkv, coef, self.num_heads, 2, self.head_size)
         # GroupLayerNorm then x(1 - lambda_init) with the MHA's own, never-updated 0.8 buffer
         gn = self.group_norm

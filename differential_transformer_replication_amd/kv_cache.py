@@ -84,9 +84,7 @@ def _constants(attn, layer: int, H: int, hs: int, bs: int, device):
     if hasattr(attn, "coefficients"):
         return attn.packed_weight(), attn.coefficients(layer), freqs
     # control.py MultiHeadAttention: packed [Q | K | V], one branch of weight 1
-    w = torch.cat([h.query.weight for h in attn.heads] + [h.key.weight for h in attn.heads]
-                  + [h.value.weight for h in attn.heads], 0)
-    return w, torch.ones(H, 1, device=device, dtype=torch.float32), freqs
+    return attn.packed_weight(), torch.ones(H, 1, device=device, dtype=torch.float32), freqs
 
 
 def _attention_step(block, x: torch.Tensor, layer: int, cache: KVCache, pos: int) -> torch.Tensor:

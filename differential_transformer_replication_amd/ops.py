@@ -145,19 +145,15 @@ class _DiffAttention(torch.autograd.Function):
         dq, dk, dvv = split_packed(dqkv, H, N, hs, dv)
         dcoef = torch.empty(H, N, device=dev, dtype=torch.float32)
         delta = torch.empty(N, B, H, T, device=dev, dtype=torch.float32)
-        rope = freqs is not None
-        # with RoPE the kernels produce gradients of the ROTATED Q/K; dQ stays fp32 for the inverse rotation
-        dq32 = torch.empty(B, T, H, N, hs, device=dev, dtype=torch.float32) if rope else None
-        dk_rot = torch.empty(B, T, H, N, hs, device=dev, dtype=qkv.dtype) if rope else None
+        # with RoPE the kernels differentiate w.r.t. the rotated Q/K (qk_rot) and their
+        # dQ / dK epilogues apply the inverse rotation, writing straight into dqkv
         obr_t = _lib.DtaTensor(obr.data_ptr(), *obr.stride()[1:4], obr.stride(0))
-        null = _lib.DtaTensor(None, 0, 0, 0, 0)
         a = _lib.AttnBwdArgs(dt, B, T, H, N, hs, dv, 1.0 / math.sqrt(hs), 0.0,
                              _lib.tensor5(q), _lib.tensor5(k), _lib.tensor5(v), obr_t,
                              lse.data_ptr(), coef.data_ptr(), _lib.tensor5(do),
-                             null if rope else _lib.tensor5(dq),
-                             _lib.tensor5(dk_rot if rope else dk), _lib.tensor5(dvv),
-                             dcoef.data_ptr(), delta.data_ptr(), dq32.data_ptr() if rope else None,
-                             _lib.BWD_PRE)
+                             _lib.tensor5(dq), _lib.tensor5(dk), _lib.tensor5(dvv),
+                             dcoef.data_ptr(), delta.data_ptr(), None, _lib.BWD_PRE,
+                             freqs.data_ptr() if freqs is not None else None)
         _lib.check(lib.dta_attn_bwd(a, stream))
         a.stages = _lib.BWD_DQ
         with TIMER.region("attn_bwd_dq"):
@@ -165,12 +161,6 @@ class _DiffAttention(torch.autograd.Function):
         a.stages = _lib.BWD_DKDV
         with TIMER.region("attn_bwd_dkdv"):
             _lib.check(lib.dta_attn_bwd(a, stream))
-        if rope:
-            # gradients back through the rotation: conjugate rotate (Ndiff_transformer.py:11-22 bwd)
-            ra = _lib.RopeArgs(dt, B, T, H, N, hs, 1, 1, _lib.tensor5(dq32), _lib.tensor5(dq), freqs.data_ptr())
-            _lib.check(lib.dta_rope(ra, stream))
-            ra = _lib.RopeArgs(dt, B, T, H, N, hs, 1, 0, _lib.tensor5(dk_rot), _lib.tensor5(dk), freqs.data_ptr())
-            _lib.check(lib.dta_rope(ra, stream))
         return dqkv, dcoef, None, None, None, None, None
 
 

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define DTA_ABI_VERSION 1
+#define DTA_ABI_VERSION 2
 
 enum dta_dtype { DTA_BF16 = 0, DTA_F16 = 1, DTA_F32 = 2 };
 
@@ -108,6 +108,12 @@ typedef struct dta_attn_bwd_args {
                                 (key-major kernel) -- lets a caller bracket one
                                 kernel with events on the same stream; DQ must
                                 run before DKDV (it produces delta) */
+  const float* rope_freqs;   /* optional fp32 [T][head_size/2][2] (cos, sin) table,
+                                16-byte aligned: q and k are the RoPE'd Q_i / K_i
+                                (Ndiff_transformer.py:104-109), and dQ / dK are
+                                returned w.r.t. the UN-rotated projections -- the
+                                inverse rotation (apply_rotary_emb's backward) runs
+                                in the kernels' epilogues, no extra pass or buffer */
 } dta_attn_bwd_args;
 
 enum { DTA_BWD_PRE = 1, DTA_BWD_DQ = 2, DTA_BWD_DKDV = 4 };

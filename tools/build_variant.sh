@@ -1,0 +1,13 @@
+# Build lib/libdiffattn_<name>.so: attn_bf16.hip compiled with extra flags (e.g. -DDTA_FWD_PINGPONG=1),
+# everything else from the regular build.   bash tools/build_variant.sh <name> "<flags>"
+set -e
+NAME=$1; EXTRA=$2
+C=$(dirname $0)/../differential_transformer_replication_amd/csrc
+make -C $C -j8 >/dev/null
+FLAGS="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -munsafe-fp-atomics -fno-honor-nans -fno-slp-vectorize -Wall -Wno-unused-function -Wno-unused-variable -Wno-unused-but-set-variable"
+mkdir -p $C/build_v
+/opt/rocm/bin/hipcc $FLAGS $EXTRA -c ${SRC:-$C/attn_bf16.hip} -o $C/build_v/attn_bf16_$NAME.o
+/opt/rocm/bin/hipcc $FLAGS $EXTRA -c $C/capi.hip -o $C/build_v/capi_$NAME.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $C/build_v/capi_$NAME.o $C/build/elementwise.o $C/build/decode.o \
+  $C/build/attn_f16.o $C/build/attn_f32.o $C/build_v/attn_bf16_$NAME.o -o $C/../lib/libdiffattn_$NAME.so
+echo built lib/libdiffattn_$NAME.so
