@@ -22,7 +22,8 @@ _DTYPES = {torch.bfloat16: DTA_BF16, torch.float16: DTA_F16, torch.float32: DTA_
 ABI_VERSION = 2
 
 # every symbol include/diffattn.h declares
-EXPORTS = ("dta_attn_fwd", "dta_attn_bwd", "dta_attn_bwd_workspace_bytes", "dta_ln_fwd", "dta_ln_bwd",
+EXPORTS = ("dta_attn_fwd", "dta_attn_bwd", "dta_attn_bwd_workspace_bytes", "dta_attn_bwd_dcoef_partial_bytes",
+           "dta_ln_fwd", "dta_ln_bwd", "dta_ln_bwd_workspace_bytes",
            "dta_rope", "dta_cast_f32", "dta_error_string", "dta_abi_version", "dta_supported",
            "dta_attn_decode", "dta_attn_decode_workspace_bytes")
 
@@ -48,7 +49,7 @@ class AttnBwdArgs(ctypes.Structure):
                 ("lse", ctypes.c_void_p), ("coef", ctypes.c_void_p), ("dout", DtaTensor),
                 ("dq", DtaTensor), ("dk", DtaTensor), ("dv_out", DtaTensor),
                 ("dcoef", ctypes.c_void_p), ("delta", ctypes.c_void_p), ("dq_f32", ctypes.c_void_p),
-                ("stages", ctypes.c_int32), ("rope_freqs", ctypes.c_void_p)]
+                ("stages", ctypes.c_int32), ("rope_freqs", ctypes.c_void_p), ("dcoef_partial", ctypes.c_void_p)]
 
 
 BWD_PRE, BWD_DQ, BWD_DKDV = 1, 2, 4
@@ -63,7 +64,7 @@ class LnArgs(ctypes.Structure):
                 ("mean", ctypes.c_void_p), ("rstd", ctypes.c_void_p),
                 ("dy", ctypes.c_void_p), ("dy_stride", ctypes.c_int64),
                 ("dx", ctypes.c_void_p), ("dx_stride", ctypes.c_int64),
-                ("dw", ctypes.c_void_p), ("db", ctypes.c_void_p)]
+                ("dw", ctypes.c_void_p), ("db", ctypes.c_void_p), ("partial", ctypes.c_void_p)]
 
 
 class RopeArgs(ctypes.Structure):
@@ -107,6 +108,10 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         lib.dta_attn_decode_workspace_bytes.restype = ctypes.c_size_t
         lib.dta_attn_bwd_workspace_bytes.argtypes = [ctypes.c_int32] * 5
         lib.dta_attn_bwd_workspace_bytes.restype = ctypes.c_size_t
+        lib.dta_attn_bwd_dcoef_partial_bytes.argtypes = [ctypes.c_int32] * 4
+        lib.dta_attn_bwd_dcoef_partial_bytes.restype = ctypes.c_size_t
+        lib.dta_ln_bwd_workspace_bytes.argtypes = [ctypes.c_int64] * 2
+        lib.dta_ln_bwd_workspace_bytes.restype = ctypes.c_size_t
         lib.dta_error_string.argtypes = [ctypes.c_int]
         lib.dta_error_string.restype = ctypes.c_char_p
         lib.dta_supported.argtypes = [ctypes.c_int32] * 4

@@ -39,6 +39,10 @@
 #ifndef DTA_DQ_AHEAD
 #define DTA_DQ_AHEAD 0
 #endif
+// dK/dV kernel: per-lane DMA source offsets computed once instead of per query tile
+#ifndef DTA_DKDV_PREOFF
+#define DTA_DKDV_PREOFF 0
+#endif
 // forward: the two waves of a SIMD run half a tile apart (see attn_fwd_kernel)
 #ifndef DTA_FWD_PINGPONG
 #define DTA_FWD_PINGPONG 0
@@ -354,7 +358,7 @@ struct KvRing {
   }
   __device__ static void issue(const E* gk, int64_t kst, int64_t ksi, const E* gv, int64_t vst, int k0, int T,
                                E* kdst, E* vdst, int wave, int lane) {
-    const int rows = T - k0;
+    const int rows = max(0, T - k0);           // a tile past T reads (as zeros) nothing
     const E* bk = gk + (int64_t)k0 * kst;
     const E* bv = gv + (int64_t)k0 * vst;
     const uint32_t nk = (uint32_t)rows * (uint32_t)(kst * ES), nv = (uint32_t)rows * (uint32_t)(vst * ES);
@@ -370,6 +374,38 @@ struct KvRing {
       } else {
         if (j < PK) buf_lds16(bk, nk, kd + j * 1024, offk(kst, ksi, j, lane));
         else if (j < NPC) buf_lds16(bv, nv, vd + (j - PK) * 1024, offv(vst, j, lane));
+      }
+    });
+  }
+  // the per-lane source offsets of this wave's pieces are the same for every tile:
+  // computed once (VGPRs), a tile then costs only its two descriptors and M0 values
+  __device__ static void offsets(int64_t kst, int64_t ksi, int64_t vst, int wave, int lane, uint32_t (&off)[MYP]) {
+    sfor<MYP>([&](auto U) {
+      constexpr int u = decltype(U)::value;
+      const int j = u * NW + wave;
+      if constexpr ((u + 1) * NW <= PK) off[u] = offk(kst, ksi, j, lane);
+      else if constexpr (u * NW >= PK && (u + 1) * NW <= NPC) off[u] = offv(vst, j, lane);
+      else off[u] = j < PK ? offk(kst, ksi, j, lane) : (j < NPC ? offv(vst, j, lane) : 0u);
+    });
+  }
+  __device__ static void issue_pre(const E* gk, int64_t kst, const E* gv, int64_t vst, int k0, int T, E* kdst,
+                                   E* vdst, int wave, const uint32_t (&off)[MYP]) {
+    const int rows = max(0, T - k0);
+    const E* bk = gk + (int64_t)k0 * kst;
+    const E* bv = gv + (int64_t)k0 * vst;
+    const uint32_t nk = (uint32_t)rows * (uint32_t)(kst * ES), nv = (uint32_t)rows * (uint32_t)(vst * ES);
+    char* kd = reinterpret_cast<char*>(kdst);
+    char* vd = reinterpret_cast<char*>(vdst);
+    sfor<MYP>([&](auto U) {
+      constexpr int u = decltype(U)::value;
+      const int j = u * NW + wave;
+      if constexpr ((u + 1) * NW <= PK) {
+        buf_lds16(bk, nk, kd + j * 1024, off[u]);
+      } else if constexpr (u * NW >= PK && (u + 1) * NW <= NPC) {
+        buf_lds16(bv, nv, vd + (j - PK) * 1024, off[u]);
+      } else {
+        if (j < PK) buf_lds16(bk, nk, kd + j * 1024, off[u]);
+        else if (j < NPC) buf_lds16(bv, nv, vd + (j - PK) * 1024, off[u]);
       }
     });
   }
@@ -797,6 +833,297 @@ __global__ __launch_bounds__(NW * 64, (FwdCfg<E, HS, N, DVC, NW, QREG>::WPE)) vo
     }
 }
 
+// --------------------------------------- forward, software-pipelined ---
+//
+// One wave per SIMD (4 waves x 32 query rows; the whole 512-entry register file),
+// Q fragments in registers, K/V tiles through a 4-stage LDS-DMA ring.  The loop
+// body is straight-line: after this tile's maxima (and the rare rescale), it
+// issues the NEXT tile's QK^T MFMAs, this tile's exp / row sums / P packing and
+// this tile's PV MFMAs in one basic block, so one wave keeps its MFMA pipe fed
+// while its own softmax VALU runs -- instead of relying on two lockstepped waves
+// per SIMD, whose VALU phases coincide at every tile barrier (measured: 36% of the
+// forward's cycles in one shared phase, tools/stamps.py).
+// Ring: tile t+3 is staged (unconditionally: past T it reads nothing) at the top of
+// iteration t into the buffer of tile t-1, whose V was last read before the barrier
+// that ended iteration t-1 and whose K before the one that ended t-2; iteration t
+// ends with tile t+2 landed (K(t+2) feeds the next iteration's QK^T).
+#ifndef DTA_FWD_PIPE_BN
+#define DTA_FWD_PIPE_BN 32   // 64: 1.088-1.133 ms, 32: 1.195 ms vs 1.02 for the 8-wave kernel (cfg2 A/B)
+#endif
+#ifndef DTA_FWD_PIPE_PINQ
+#define DTA_FWD_PIPE_PINQ 0
+#endif
+template <class E, int HS, int N, int DVC>
+struct FwdPipeCfg {
+  static constexpr int NW = 4, BM = NW * 32, BN = DTA_FWD_PIPE_BN, NKB = BN / 32;
+  static constexpr int nK = N * BN * HS, nV = BN * DVC;
+  static constexpr int NS = 4;
+  static constexpr int bytes = NS * (nK + nV) * (int)sizeof(E);
+  // O accumulators, two score tiles, Q fragments, P, K operand reads, misc
+  static constexpr int regs = N * DVC / 2 + 2 * N * NKB * 16 + N * HS / 4 + N * NKB * 8 + NKB * HS / 2 + 64;
+  static constexpr bool ok = sizeof(E) == 2 && HS >= 32 && bytes <= 160 * 1024 && regs <= 480 &&
+                             KvRing<E, HS, N, DVC, BN, NW>::ok;
+};
+
+template <class E, int HS, int N, int DVC>
+__global__ __launch_bounds__(256, 1) void attn_fwd_pipe_kernel(FwdParams p) {
+  using O = Ops<E>;
+  using frag = typename O::frag;
+  using KI = Img<E, HS>;
+  using VI = Img<E, DVC>;
+  using CF = FwdPipeCfg<E, HS, N, DVC>;
+  constexpr int NW = CF::NW, BN = CF::BN, BM = CF::BM, NS = CF::NS;
+  constexpr int KS = O::KSTEP, NSQ = HS / KS, NKB = CF::NKB, NDB = DVC / 32;
+  constexpr float THR = 8.f;        // deferred-rescale threshold (log2 units): P <= 2^8
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  E* Kb = reinterpret_cast<E*>(smem);     // [NS][N][BN][HS]
+  E* Vb = Kb + NS * CF::nK;               // [NS][BN][DVC]
+
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63, hf = lane >> 5, c32 = lane & 31;
+  const int nblk = gridDim.x * gridDim.y * gridDim.z;
+  const int lin = xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z), nblk);
+  const int bx = lin % gridDim.x, by = (lin / gridDim.x) % gridDim.y, bz = lin / (gridDim.x * gridDim.y);
+  const int nch = p.DV / DVC;
+  const int qt = gridDim.x - 1 - bx;                   // longest causal rows first
+  const int hh = by / nch, dc0 = (by % nch) * DVC;
+  const int b = bz;
+  const int T = p.T;
+  const int q0 = qt * BM, qw0 = q0 + wave * 32;
+  const int qrow = qw0 + c32;
+
+  const E* gq = reinterpret_cast<const E*>(p.q.p) + b * p.q.sb + hh * p.q.sh;
+  const E* gk = reinterpret_cast<const E*>(p.k.p) + b * p.k.sb + hh * p.k.sh;
+  const E* gv = reinterpret_cast<const E*>(p.v.p) + b * p.v.sb + hh * p.v.sh + dc0;
+  float coef[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) coef[i] = p.coef[hh * N + i];
+
+  // this wave's query rows as B fragments of S^T = K Q^T (rows past T read as zeros)
+  frag qf[N][NSQ];
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+#pragma unroll
+    for (int s = 0; s < NSQ; ++s)
+      qf[i][s] = qrow < T ? O::load_global(gq + (int64_t)qrow * p.q.st + i * p.q.si + s * KS + hf * O::KH) : O::zero();
+
+  const int kend = min(T, q0 + BM);
+  const int ntiles = (kend + BN - 1) / BN;
+  using KR = KvRing<E, HS, N, DVC, BN, NW>;
+  const int pieces = KR::pieces(wave);
+  uint32_t doff[KR::MYP];
+  KR::offsets(p.k.st, p.k.si, p.v.st, wave, lane, doff);
+  auto stage_kv = [&](int kt) {
+    const int buf = kt % NS;
+    KR::issue_pre(gk, p.k.st, gv, p.v.st, kt * BN, T, Kb + buf * N * BN * HS, Vb + buf * BN * DVC, wave, doff);
+  };
+#pragma unroll
+  for (int j = 0; j < NS - 1; ++j) stage_kv(j);
+  wait_vm(pieces);                       // tiles 0 and 1 landed (tile 2 may fly)
+  lds_barrier();
+
+  f32x16 acc[N][NDB];
+  float m[N], l[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    m[i] = -INFINITY;
+    l[i] = 0.f;
+#pragma unroll
+    for (int d = 0; d < NDB; ++d) acc[i][d] = f32x16{};
+  }
+  // O accumulators and Q fragments are MFMA operands only: keep them in AGPRs, the
+  // VGPRs for the two score tiles the softmax VALU works on
+  auto pin = [&]() {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+#pragma unroll
+      for (int d = 0; d < NDB; ++d) asm volatile("" : "+a"(acc[i][d]));
+      if constexpr (DTA_FWD_PIPE_PINQ) {
+#pragma unroll
+        for (int s = 0; s < NSQ; ++s) asm volatile("" : "+a"(qf[i][s]));
+      }
+    }
+  };
+  pin();
+
+  // S^T of tile kt for every branch (all operand reads ahead of each branch's chain)
+  auto qk = [&](int kt, f32x16 (&sc)[N][NKB]) {
+    const char* kbase = reinterpret_cast<const char*>(Kb + (kt % NS) * N * BN * HS);
+    const int Lr = row_lane<KI::ROWB>(lane);
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      frag kfr[NKB][NSQ];
+#pragma unroll
+      for (int s = 0; s < NSQ; ++s)
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb)
+          kfr[kb][s] = *reinterpret_cast<const frag*>(kbase + (i * BN + kb * 32) * KI::ROWB + (Lr ^ (32 * s)));
+#pragma unroll
+      for (int kb = 0; kb < NKB; ++kb) sc[i][kb] = f32x16{};
+#pragma unroll
+      for (int s = 0; s < NSQ; ++s)
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb) sc[i][kb] = O::mma(kfr[kb][s], qf[i][s], sc[i][kb]);
+    }
+  };
+
+  f32x16 sa[N][NKB], sb[N][NKB];
+  float mx[N];                           // scale*log2e * row max of the pending tile's scores, per branch
+  // mask (diagonal / past-T tiles) and row maxima of tile kt's raw scores
+  auto mask_max = [&](int kt, auto MASKED, f32x16 (&sc)[N][NKB]) {
+    const int k0 = kt * BN;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      if constexpr (decltype(MASKED)::value) {
+        const int lim = min(qrow, T - 1) - k0 - 4 * hf;     // key > qrow or key >= T: masked
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            sc[i][kb][r] = (kb * 32 + (r & 3) + 8 * (r >> 2) > lim) ? -INFINITY : sc[i][kb][r];
+      }
+      float a = -INFINITY, c = -INFINITY;
+#pragma unroll
+      for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; r += 4) {
+          a = fmaxf(fmaxf(a, sc[i][kb][r]), sc[i][kb][r + 1]);
+          c = fmaxf(fmaxf(c, sc[i][kb][r + 2]), sc[i][kb][r + 3]);
+        }
+      mx[i] = wave_max_halves(fmaxf(a, c)) * p.sl2;
+    }
+  };
+  const int nunm = min(ntiles, min((q0 + 1) / BN, T / BN));       // tiles that need no mask
+  qk(0, sa);
+  if (nunm > 0) mask_max(0, std::false_type{}, sa);
+  else mask_max(0, std::true_type{}, sa);
+
+  Stamps st;
+  // iteration kt: rescale decision for tile kt (maxima from the previous block), then ONE
+  // straight-line block: stage tile kt+3, QK^T of tile kt+1, exp / pack / PV of tile kt,
+  // then mask + maxima of tile kt+1 (its MFMAs have drained behind this tile's PV)
+  auto iter = [&](int kt, auto MASKNEXT, auto NEXT, f32x16 (&sc)[N][NKB], f32x16 (&sn)[N][NKB]) {
+    constexpr bool HAS_NEXT = decltype(NEXT)::value;
+    bool grow = false;
+#pragma unroll
+    for (int i = 0; i < N; ++i) grow = grow || mx[i] > m[i] + THR;
+    if (__any(grow)) {
+      asm volatile("" ::: "memory");     // a real (rare) branch, never speculated into every tile
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        const float mnew = fmaxf(m[i], mx[i]);
+        const float alpha = exp2_fast(m[i] - mnew);
+        m[i] = mnew;
+        l[i] *= alpha;
+#pragma unroll
+        for (int d = 0; d < NDB; ++d) acc[i][d] *= alpha;
+      }
+    }
+    st.lap<0>();
+    stage_kv(kt + NS - 1);
+    st.lap<1>();
+    if constexpr (HAS_NEXT) qk(kt + 1, sn);
+    frag pf[N][NKB * 2];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const float mi = m[i];
+      float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+      for (int kb = 0; kb < NKB; ++kb) {
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+          const float e0 = exp2_fast(fmaf(sc[i][kb][r], p.sl2, -mi));
+          const float e1 = exp2_fast(fmaf(sc[i][kb][r + 1], p.sl2, -mi));
+          sc[i][kb][r] = e0;
+          sc[i][kb][r + 1] = e1;
+          s0 += e0;
+          s1 += e1;
+        }
+        pf[i][kb * 2 + 0] = O::template pack<0>(sc[i][kb]);
+        pf[i][kb * 2 + 1] = O::template pack<1>(sc[i][kb]);
+      }
+      l[i] += s0 + s1;
+    }
+    {
+      const unsigned vb = lds_addr(Vb + (kt % NS) * BN * DVC);
+      const int Lv = tr_lane<VI::ROWB>(lane);
+      sfor<NDB>([&](auto D) {
+        constexpr int d = decltype(D)::value;
+        lds64 r[NKB][4];
+        const unsigned a0 = vb + (Lv ^ (64 * d)), a1 = vb + (Lv ^ (64 * d + 32));
+        sfor<NKB>([&](auto KB) { tr_issue<VI::ROWB, 32 * decltype(KB)::value>(r[decltype(KB)::value], a0, a1); });
+        lgkm_pin<NKB>(r);
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            const frag va = tr_frag<E>(r[kb], s);
+#pragma unroll
+            for (int i = 0; i < N; ++i) acc[i][d] = O::mma(va, pf[i][kb * 2 + s], acc[i][d]);
+          }
+      });
+    }
+    if constexpr (HAS_NEXT) mask_max(kt + 1, MASKNEXT, sn);
+    pin();
+    st.lap<2>();
+    wait_vm(pieces);                     // tile kt+2 landed; tile kt+3 may fly
+    st.lap<3>();
+    lds_barrier();
+    st.lap<4>();
+  };
+  auto copy_scores = [&]() {
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+#pragma unroll
+      for (int kb = 0; kb < NKB; ++kb) sa[i][kb] = sb[i][kb];
+  };
+  const std::true_type Y{};
+  const std::false_type F{};
+  // iterations whose NEXT tile needs no mask: kt + 1 < nunm
+  const int n1 = max(0, min(ntiles - 1, nunm - 1));
+  int kt = 0;
+  st.start();
+  // two at a time, the score tiles alternating (no register copies)
+  for (; kt + 2 <= n1; kt += 2) {
+    iter(kt, F, Y, sa, sb);
+    iter(kt + 1, F, Y, sb, sa);
+  }
+  for (; kt < n1; ++kt) { iter(kt, F, Y, sa, sb); copy_scores(); }
+  for (; kt < ntiles - 1; ++kt) { iter(kt, Y, Y, sa, sb); copy_scores(); }
+  if (ntiles > 0) iter(ntiles - 1, Y, F, sa, sb);
+  wait_vm(0);                            // no LDS-DMA left in flight at exit
+  st.flush(p.stamps, lin * NW + wave, lane);
+
+  if (qw0 >= T || qrow >= T) return;
+  float inv[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const float lt = wave_sum_halves(l[i]);
+    inv[i] = 1.f / lt;
+    if (dc0 == 0 && hf == 0)
+      p.lse[(((int64_t)i * p.B + b) * p.H + hh) * T + qrow] = -(m[i] + __builtin_log2f(lt));   // stored negated
+  }
+  E* go = reinterpret_cast<E*>(p.o.p) + b * p.o.sb + (int64_t)qrow * p.o.st + hh * p.o.sh + dc0;
+  E* gob = reinterpret_cast<E*>(p.obr.p) + b * p.obr.sb + (int64_t)qrow * p.obr.st + hh * p.obr.sh + dc0;
+#pragma unroll
+  for (int d = 0; d < NDB; ++d)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int e = d * 32 + 8 * g + 4 * hf;
+      float o0 = 0.f, o1 = 0.f, o2 = 0.f, o3 = 0.f;
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        const float a0 = acc[i][d][4 * g + 0] * inv[i], a1 = acc[i][d][4 * g + 1] * inv[i];
+        const float a2 = acc[i][d][4 * g + 2] * inv[i], a3 = acc[i][d][4 * g + 3] * inv[i];
+        store4<E>(gob + i * p.obr.si + e, a0, a1, a2, a3);
+        o0 = fmaf(coef[i], a0, o0); o1 = fmaf(coef[i], a1, o1);
+        o2 = fmaf(coef[i], a2, o2); o3 = fmaf(coef[i], a3, o3);
+      }
+      store4<E>(go + e, o0, o1, o2, o3);
+    }
+}
+
 // ------------------------------------------------------ backward: dQ ---
 template <class E, int HS, int N, int DV, int NW, bool QREG>
 struct DqCfg {
@@ -916,7 +1243,12 @@ void attn_dq_kernel(BwdParams p) {
     float w = (rowok && hf == 0) ? d : 0.f;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) w += __shfl_xor(w, o, 64);
-    if (lane == 0 && qw0 < T) atomicAdd(p.dcoef + hh * N + i, w);
+    if (p.dcoef_part) {
+      // one slot per (h, i, b, 32-row block): every slot written once, summed in order later
+      if (lane == 0 && qw0 < T) p.dcoef_part[(((int64_t)hh * N + i) * p.B + b) * ((T + 31) / 32) + qw0 / 32] = w;
+    } else if (lane == 0 && qw0 < T) {
+      atomicAdd(p.dcoef + hh * N + i, w);
+    }
   }
 
   if constexpr (!QREG) {
@@ -1155,6 +1487,38 @@ struct TileRing {
       }
     });
   }
+  // per-lane source offsets of this wave's pieces: the same for every tile (VGPRs, once)
+  __device__ static void offsets(const BwdParams& p, int64_t bstride, int wave, int lane, uint32_t (&off)[MYP]) {
+    sfor<MYP>([&](auto U) {
+      constexpr int u = decltype(U)::value;
+      const int j = u * NW + wave;
+      if constexpr ((u + 1) * NW <= PQ) off[u] = offq(p, j, lane);
+      else if constexpr (u * NW >= PQ && (u + 1) * NW <= PQ + PD) off[u] = offd(p, j, lane);
+      else off[u] = j < PQ ? offq(p, j, lane) : (j < PQ + PD ? offd(p, j, lane) : (j < NPC ? offr(j, lane, bstride) : 0u));
+    });
+  }
+  __device__ static void issue_pre(const BwdParams& p, const E* gq, const E* gdo, const float* lse, const float* delta,
+                                   int64_t bstride, int q0, int T, char* st0, int wave, const uint32_t (&off)[MYP]) {
+    const int rows = T - q0;
+    const E* bq = gq + (int64_t)q0 * p.q.st;
+    const E* bd = gdo + (int64_t)q0 * p.dout.st;
+    const uint32_t nq = (uint32_t)rows * (uint32_t)(p.q.st * ES), nd = (uint32_t)rows * (uint32_t)(p.dout.st * ES);
+    const uint32_t nl = (uint32_t)(((N - 1) * bstride + rows) * 4);
+    sfor<MYP>([&](auto U) {
+      constexpr int u = decltype(U)::value;
+      const int j = u * NW + wave;
+      if constexpr ((u + 1) * NW <= PQ) {
+        buf_lds16(bq, nq, st0 + j * 1024, off[u]);
+      } else if constexpr (u * NW >= PQ && (u + 1) * NW <= PQ + PD) {
+        buf_lds16(bd, nd, st0 + OFF_D + (j - PQ) * 1024, off[u]);
+      } else {
+        if (j < PQ) buf_lds16(bq, nq, st0 + j * 1024, off[u]);
+        else if (j < PQ + PD) buf_lds16(bd, nd, st0 + OFF_D + (j - PQ) * 1024, off[u]);
+        else if (j < PQ + PD + PL) buf_lds4(lse + q0, nl, st0 + OFF_L + (j - PQ - PD) * 256, off[u]);
+        else if (j < NPC) buf_lds4(delta + q0, nl, st0 + OFF_G + (j - PQ - PD - PL) * 256, off[u]);
+      }
+    });
+  }
 };
 
 // The buffer descriptors cover [row base, T rows) of each operand: every branch's
@@ -1263,8 +1627,12 @@ __global__ __launch_bounds__(NW * 64, (NW >= 8 ? 2 : 1)) void attn_dkdv_kernel(B
       vf[s] = krow < T ? O::load_global(gv + (int64_t)krow * p.v.st + s * KS + hf * O::KH) : O::zero();
   }
 
+  uint32_t roff[SRD && DTA_DKDV_PREOFF ? RG::MYP : 1];
+  if constexpr (SRD && DTA_DKDV_PREOFF) RG::offsets(p, bstride, wave, lane, roff);
   auto stage_q = [&](int q0, int buf) {
-    if constexpr (SRD) {
+    if constexpr (SRD && DTA_DKDV_PREOFF) {
+      RG::issue_pre(p, gq, gdo, p.lse + rowvec, p.delta + rowvec, bstride, q0, T, ringb + buf * RG::SB, wave, roff);
+    } else if constexpr (SRD) {
       RG::issue(p, gq, gdo, p.lse + rowvec, p.delta + rowvec, bstride, q0, T, ringb + buf * RG::SB, wave, lane);
     } else {
 #pragma unroll
@@ -1781,11 +2149,33 @@ struct Plan {
   static constexpr bool ok = FP::ok && DP::ok && DkdvCfg<E, HS, N, DV, KVW>::bytes <= 160 * 1024;
 };
 
+// forward kernel choice: DTA_FWD_PIPE=1 (env) or -DDTA_FWD_PIPE_DEFAULT=1 selects the
+// software-pipelined one-wave-per-SIMD kernel where its plan fits
+#ifndef DTA_FWD_PIPE_DEFAULT
+#define DTA_FWD_PIPE_DEFAULT 0
+#endif
+inline bool fwd_pipe() {
+  static const bool on = [] {
+    const char* s = getenv("DTA_FWD_PIPE");
+    return s ? s[0] == '1' : DTA_FWD_PIPE_DEFAULT != 0;
+  }();
+  return on;
+}
+
 template <class E, int HS, int N, int DV_>
 int launch_fwd_t(const FwdParams& p, hipStream_t st) {
   using PL = Plan<E, HS, N, DV_>;
   using FP = typename PL::FP;
   constexpr int DVC = FP::DVC, NW = FP::NW;
+  if constexpr (FwdPipeCfg<E, HS, N, DVC>::ok) {
+    if (fwd_pipe() && kv_layout_ok(p, (int)sizeof(E))) {
+      using PC = FwdPipeCfg<E, HS, N, DVC>;
+      auto kern = attn_fwd_pipe_kernel<E, HS, N, DVC>;
+      if (int e = set_smem(kern, PC::bytes)) return e;
+      hipLaunchKernelGGL(kern, dim3((p.T + PC::BM - 1) / PC::BM, p.H * (PL::DV / DVC), p.B), dim3(256), PC::bytes, st, p);
+      return (int)hipGetLastError();
+    }
+  }
   constexpr int bytes = FwdCfg<E, HS, N, DVC, NW, FP::QREG>::bytes;
   dim3 grid((p.T + NW * 32 - 1) / (NW * 32), p.H * (PL::DV / DVC), p.B);
   auto run = [&](auto SRDV) -> int {

@@ -163,6 +163,10 @@ int dta_attn_fwd(const dta_attn_fwd_args* a, void* stream) {
   return status(launch_attn_fwd(a->dtype, p, (hipStream_t)stream));
 }
 
+size_t dta_attn_bwd_dcoef_partial_bytes(int32_t B, int32_t T, int32_t H, int32_t n_terms) {
+  return (size_t)H * n_terms * B * ((T + 31) / 32) * 4;
+}
+
 size_t dta_attn_bwd_workspace_bytes(int32_t B, int32_t T, int32_t H, int32_t n_terms, int32_t head_size) {
   const size_t delta = (size_t)n_terms * B * H * T * 4;
   const size_t dq = (size_t)B * T * H * n_terms * head_size * 4;
@@ -194,12 +198,17 @@ int dta_attn_bwd(const dta_attn_bwd_args* a, void* stream) {
   p.dq32 = a->dq.ptr ? nullptr : a->dq_f32;
   if (a->rope_freqs && (a->head_size % 4 || reinterpret_cast<uintptr_t>(a->rope_freqs) % 16)) return DTA_ERR_INVALID;
   p.rope = a->rope_freqs;
+  if (a->dcoef_partial && !aligned_ptr(a->dcoef_partial)) return DTA_ERR_INVALID;
+  p.dcoef_part = a->dcoef_partial;
   p.B = a->B; p.T = a->T; p.H = a->H; p.N = a->n_terms; p.HS = a->head_size; p.DV = a->dv;
   p.scale = a->scale; p.sl2 = a->scale * kLog2e;
   p.prio = wave_prio();
   p.stamps = stamp_buf();
   int e = 0;
   if ((stages & DTA_BWD_DQ) && (e = launch_attn_dq(a->dtype, p, st))) return status(e);
+  if ((stages & DTA_BWD_DQ) && p.dcoef_part &&
+      (e = launch_dcoef_reduce(p.dcoef_part, p.dcoef, p.H, p.N, (int64_t)p.B * ((p.T + 31) / 32), st)))
+    return status(e);
   if ((stages & DTA_BWD_DKDV) && (e = launch_attn_dkdv(a->dtype, p, st))) return status(e);
   return DTA_OK;
 }
@@ -222,6 +231,7 @@ static LnParams ln_params(const dta_ln_args* a) {
   p.w = a->w; p.b = a->b; p.mean = a->mean; p.rstd = a->rstd;
   p.dy = a->dy; p.dys = a->dy_stride; p.dx = a->dx; p.dxs = a->dx_stride;
   p.dw = a->dw; p.db = a->db;
+  p.partial = a->partial;
   return p;
 }
 
@@ -229,6 +239,8 @@ int dta_ln_fwd(const dta_ln_args* a, void* stream) {
   if (int e = ln_common(a, false)) return e;
   return status(launch_ln(a->dtype, ln_params(a), false, (hipStream_t)stream));
 }
+
+size_t dta_ln_bwd_workspace_bytes(int64_t rows, int64_t C) { return (size_t)ln_bwd_workspace_floats(rows, C) * 4; }
 
 int dta_ln_bwd(const dta_ln_args* a, void* stream) {
   if (int e = ln_common(a, true)) return e;

@@ -29,6 +29,7 @@ struct BwdParams {
   float* dcoef;        // accumulated by attn_dq (zeroed first)
   float* dq32;         // if set: dQ written as fp32 [b][t][h][i][d] instead of into dq
   const float* rope;   // if set: fp32 [T][HS/2][2] table; dQ / dK leave through the inverse rotation
+  float* dcoef_part;   // if set: per-wave d(coef) partials [h][i][b][T/32] (no atomics), summed by dcoef_reduce
   int B, T, H, N, HS, DV;
   float sl2, scale;
   int prio;            // as FwdParams::prio
@@ -51,7 +52,10 @@ struct LnParams {
   const void* dy; int64_t dys;
   void* dx; int64_t dxs;
   float* dw; float* db;
+  float* partial;      // optional [blocks][2][C] workspace: deterministic dw/db (no atomics)
 };
+int ln_bwd_blocks(int64_t rows);
+int64_t ln_bwd_workspace_floats(int64_t rows, int64_t C);
 
 struct RopeParams {
   T5 src, dst;
@@ -85,6 +89,7 @@ int launch_ln(int dtype, const LnParams& p, bool bwd, hipStream_t st);
 int launch_rope(int dtype, bool src_f32, const RopeParams& p, hipStream_t st);
 int launch_delta(int dtype, const DeltaParams& p, hipStream_t st);
 int launch_dcoef(const float* delta, float* dcoef, int B, int T, int H, int N, hipStream_t st);
+int launch_dcoef_reduce(const float* part, float* dcoef, int H, int N, int64_t per, hipStream_t st);
 int launch_cast(int dtype, const float* src, const T5& dst, int B, int T, int H, int N, int HS, hipStream_t st);
 
 }  // namespace dta

@@ -97,6 +97,24 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(LnParams p) {
   }
 }
 
+// Backward: dx per row plus per-column dw/db partial sums.  Each wave walks rows with
+// a stride, the NEXT row's x / dy loads issued before the current row's math (two rows
+// in flight per wave); the block's four waves combine their column partials in LDS.
+// Partials go either to p.partial ([block][2][C], plain stores; ln_bwd_reduce then
+// sums them in a fixed order -- bitwise reproducible) or, without a workspace,
+// straight to dw/db by atomics.
+template <class E> struct Raw8 { typedef s16x8 t; };
+template <> struct Raw8<float> { typedef f32x4 t[2]; };
+
+template <class E>
+__device__ __forceinline__ void raw_ld(const E* p, s16x8& v) { v = *reinterpret_cast<const s16x8*>(p); }
+template <class E>
+__device__ __forceinline__ void raw_cvt(const s16x8& v, float* f) {
+  const typename Vec8<E>::t w = __builtin_bit_cast(typename Vec8<E>::t, v);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] = (float)w[j];
+}
+
 template <class E, int CH>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(LnParams p) {
   const int lane = threadIdx.x & 63;
@@ -112,28 +130,55 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnParams p) {
     }
   }
   const float inv_c = 1.f / (float)p.C;
-  for (int64_t row = (int64_t)blockIdx.x * 4 + wave; row < p.rows; row += (int64_t)gridDim.x * 4) {
-    const E* x = reinterpret_cast<const E*>(p.x) + row * p.xs;
-    const E* dy = reinterpret_cast<const E*>(p.dy) + row * p.dys;
+  const int64_t stride = (int64_t)gridDim.x * 4;
+  int64_t row = (int64_t)blockIdx.x * 4 + wave;
+  // 16-bit rows stay packed in registers until used; fp32 rows are loaded as floats
+  constexpr bool P16 = sizeof(E) == 2;
+  s16x8 xr[P16 ? CH : 1], dr[P16 ? CH : 1];
+  auto load = [&](int64_t r) {
+    if constexpr (P16) {
+      const E* x = reinterpret_cast<const E*>(p.x) + r * p.xs;
+      const E* dy = reinterpret_cast<const E*>(p.dy) + r * p.dys;
+#pragma unroll
+      for (int c = 0; c < CH; ++c) {
+        const int col = (c * 64 + lane) * 8;
+        if (col < p.C) { raw_ld<E>(x + col, xr[c]); raw_ld<E>(dy + col, dr[c]); }
+      }
+    }
+  };
+  if (row < p.rows) load(row);
+  for (; row < p.rows; row += stride) {
+    float xv[CH][8], dv[CH][8];
+    if constexpr (P16) {
+#pragma unroll
+      for (int c = 0; c < CH; ++c) { raw_cvt<E>(xr[c], xv[c]); raw_cvt<E>(dr[c], dv[c]); }
+      if (row + stride < p.rows) load(row + stride);          // next row in flight during this row's math
+    } else {
+      const E* x = reinterpret_cast<const E*>(p.x) + row * p.xs;
+      const E* dy = reinterpret_cast<const E*>(p.dy) + row * p.dys;
+#pragma unroll
+      for (int c = 0; c < CH; ++c) {
+        const int col = (c * 64 + lane) * 8;
+        if (col < p.C) { ld8<E>(x + col, xv[c]); ld8<E>(dy + col, dv[c]); }
+      }
+    }
     const float mean = p.mean[row], rstd = p.rstd[row];
-    float xh[CH][8], g[CH][8];
     float sg = 0.f, sgx = 0.f;
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
       const int col = (c * 64 + lane) * 8;
       if (col < p.C) {
-        float xv[8], dv[8];
-        ld8<E>(x + col, xv);
-        ld8<E>(dy + col, dv);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          xh[c][j] = (xv[j] - mean) * rstd;
-          const float dys = dv[j] * p.out_scale;
-          dwp[c][j] = fmaf(dys, xh[c][j], dwp[c][j]);
+          const float xh = (xv[c][j] - mean) * rstd;
+          const float dys = dv[c][j] * p.out_scale;
+          dwp[c][j] = fmaf(dys, xh, dwp[c][j]);
           dbp[c][j] += dys;
-          g[c][j] = dv[j] * wv[c][j];
-          sg += g[c][j];
-          sgx = fmaf(g[c][j], xh[c][j], sgx);
+          const float g = dv[c][j] * wv[c][j];
+          xv[c][j] = xh;
+          dv[c][j] = g;
+          sg += g;
+          sgx = fmaf(g, xh, sgx);
         }
       }
     }
@@ -145,16 +190,15 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnParams p) {
       if (col < p.C) {
         float o[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = rstd * (g[c][j] - mg - xh[c][j] * mgx);
+        for (int j = 0; j < 8; ++j) o[j] = rstd * (dv[c][j] - mg - xv[c][j] * mgx);
         st8<E>(dx + col, o);
       }
     }
   }
-  // column partials: reduce the 4 waves through LDS, then one atomic per column per block
+  // column partials: reduce the 4 waves through LDS, then one value per column per block
   __shared__ float red[2][4][512];
 #pragma unroll
   for (int c = 0; c < CH; ++c) {
-    const int col0 = (c * 64 + lane) * 8;
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -166,12 +210,38 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnParams p) {
       const int which = e >> 9, k = e & 511;
       const int col = c * 512 + k;
       if (col < p.C) {
-        const float s = red[which][0][k] + red[which][1][k] + red[which][2][k] + red[which][3][k];
-        atomicAdd((which ? p.db : p.dw) + col, s);
+        const float sum = red[which][0][k] + red[which][1][k] + red[which][2][k] + red[which][3][k];
+        if (p.partial) p.partial[((int64_t)blockIdx.x * 2 + which) * p.C + col] = sum;
+        else atomicAdd((which ? p.db : p.dw) + col, sum);
       }
     }
-    (void)col0;
   }
+}
+
+// dw / db += the column sums of the per-block partials, in a fixed order: pass 1 sums
+// each of kLnChunks contiguous runs of blocks per column (many threads in flight),
+// pass 2 adds the kLnChunks run sums in order
+constexpr int kLnChunks = 32;
+__global__ __launch_bounds__(256) void ln_bwd_reduce1_kernel(const float* part, int nblk, int64_t C, float* part2) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;      // over 2 * C
+  if (e >= 2 * C) return;
+  const int which = (int)(e / C);
+  const int64_t col = e % C;
+  const int per = (nblk + kLnChunks - 1) / kLnChunks;
+  const int b0 = blockIdx.y * per, b1 = min(nblk, b0 + per);
+  float s = 0.f;
+#pragma unroll 8
+  for (int b = b0; b < b1; ++b) s += part[((int64_t)b * 2 + which) * C + col];
+  part2[(int64_t)blockIdx.y * 2 * C + e] = s;
+}
+__global__ __launch_bounds__(256) void ln_bwd_reduce2_kernel(const float* part2, int64_t C, float* dw, float* db) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= 2 * C) return;
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < kLnChunks; ++j) s += part2[(int64_t)j * 2 * C + e];
+  const int64_t col = e % C;
+  (e >= C ? db : dw)[col] += s;
 }
 
 
@@ -269,15 +339,29 @@ static inline int grid_for(int64_t items) {
   return (int)(g > 16384 ? 16384 : (g < 1 ? 1 : g));
 }
 
+// blocks of the LN backward: enough waves in flight to cover HBM latency, few enough
+// that the per-block column partials stay small (dta_ln_bwd_workspace_bytes)
+int ln_bwd_blocks(int64_t rows) { return (int)std::min<int64_t>((rows + 7) / 8, 1024); }
+int64_t ln_bwd_workspace_floats(int64_t rows, int64_t C) { return ((int64_t)ln_bwd_blocks(rows) + kLnChunks) * 2 * C; }
+
 template <class E>
 int ln_launch(const LnParams& p, bool bwd, hipStream_t st) {
   const int64_t ch = (p.C + 511) / 512;
   const int fwd_grid = (int)((p.rows + 3) / 4);
-  const int bwd_grid = (int)std::min<int64_t>((p.rows + 3) / 4, 2048);
+  const int bwd_grid = ln_bwd_blocks(p.rows);
 #define DTA_LN(CH_)                                                                    \
   if (ch <= CH_) {                                                                     \
-    if (bwd) hipLaunchKernelGGL((ln_bwd_kernel<E, CH_>), dim3(bwd_grid), dim3(256), 0, st, p); \
-    else hipLaunchKernelGGL((ln_fwd_kernel<E, CH_>), dim3(fwd_grid), dim3(256), 0, st, p);     \
+    if (bwd) {                                                                         \
+      hipLaunchKernelGGL((ln_bwd_kernel<E, CH_>), dim3(bwd_grid), dim3(256), 0, st, p); \
+      if (p.partial) {                                                                 \
+        float* part2 = p.partial + (int64_t)bwd_grid * 2 * p.C;                        \
+        const unsigned g = (unsigned)((2 * p.C + 255) / 256);                          \
+        hipLaunchKernelGGL(ln_bwd_reduce1_kernel, dim3(g, kLnChunks), dim3(256), 0, st, p.partial, bwd_grid, p.C, part2); \
+        hipLaunchKernelGGL(ln_bwd_reduce2_kernel, dim3(g), dim3(256), 0, st, part2, p.C, p.dw, p.db); \
+      }                                                                                \
+    } else {                                                                           \
+      hipLaunchKernelGGL((ln_fwd_kernel<E, CH_>), dim3(fwd_grid), dim3(256), 0, st, p); \
+    }                                                                                  \
     return (int)hipGetLastError();                                                     \
   }
   DTA_LN(1) DTA_LN(2) DTA_LN(4) DTA_LN(8) DTA_LN(16)
@@ -329,6 +413,23 @@ int launch_delta(int dtype, const DeltaParams& p, hipStream_t st) {
 
 int launch_dcoef(const float* delta, float* dcoef, int B, int T, int H, int N, hipStream_t st) {
   hipLaunchKernelGGL(dcoef_kernel, dim3(H * N), dim3(256), 0, st, delta, dcoef, B, T, H, N);
+  return (int)hipGetLastError();
+}
+
+// dcoef[h][i] = sum of the dQ kernel's per-wave partials part[h][i][0..per), in order
+__global__ __launch_bounds__(256) void dcoef_reduce_kernel(const float* part, float* dcoef, int64_t per) {
+  const float* src = part + (int64_t)blockIdx.x * per;
+  float s = 0.f;
+  for (int64_t t = threadIdx.x; t < per; t += 256) s += src[t];
+  s = wave_sum(s);
+  __shared__ float w4[4];
+  if ((threadIdx.x & 63) == 0) w4[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) dcoef[blockIdx.x] = (w4[0] + w4[1]) + (w4[2] + w4[3]);
+}
+
+int launch_dcoef_reduce(const float* part, float* dcoef, int H, int N, int64_t per, hipStream_t st) {
+  hipLaunchKernelGGL(dcoef_reduce_kernel, dim3(H * N), dim3(256), 0, st, part, dcoef, per);
   return (int)hipGetLastError();
 }
 

@@ -145,6 +145,8 @@ class _DiffAttention(torch.autograd.Function):
         dq, dk, dvv = split_packed(dqkv, H, N, hs, dv)
         dcoef = torch.empty(H, N, device=dev, dtype=torch.float32)
         delta = torch.empty(N, B, H, T, device=dev, dtype=torch.float32)
+        # d(coef) from per-wave partials summed in a fixed order: reproducible lambda grads
+        dcp = torch.empty(lib.dta_attn_bwd_dcoef_partial_bytes(B, T, H, N) // 4, device=dev, dtype=torch.float32)
         # with RoPE the kernels differentiate w.r.t. the rotated Q/K (qk_rot) and their
         # dQ / dK epilogues apply the inverse rotation, writing straight into dqkv
         obr_t = _lib.DtaTensor(obr.data_ptr(), *obr.stride()[1:4], obr.stride(0))
@@ -153,7 +155,7 @@ class _DiffAttention(torch.autograd.Function):
                              lse.data_ptr(), coef.data_ptr(), _lib.tensor5(do),
                              _lib.tensor5(dq), _lib.tensor5(dk), _lib.tensor5(dvv),
                              dcoef.data_ptr(), delta.data_ptr(), None, _lib.BWD_PRE,
-                             freqs.data_ptr() if freqs is not None else None)
+                             freqs.data_ptr() if freqs is not None else None, dcp.data_ptr())
         _lib.check(lib.dta_attn_bwd(a, stream))
         a.stages = _lib.BWD_DQ
         with TIMER.region("attn_bwd_dq"):
@@ -210,9 +212,11 @@ class _GroupLNScale(torch.autograd.Function):
         dx = torch.empty_like(x2)
         dw = torch.zeros(C, device=x2.device, dtype=torch.float32)
         db = torch.zeros(C, device=x2.device, dtype=torch.float32)
+        # per-block column partials summed in order: reproducible dw / db (no atomics)
+        part = torch.empty(lib.dta_ln_bwd_workspace_bytes(x2.shape[0], C) // 4, device=x2.device, dtype=torch.float32)
         a = _lib.LnArgs(_lib.dtype_code(x2.dtype), x2.shape[0], C, eps, out_scale, x2.data_ptr(), C, None, 0,
                         w32.data_ptr(), None, mean.data_ptr(), rstd.data_ptr(), dy2.data_ptr(), C,
-                        dx.data_ptr(), C, dw.data_ptr(), db.data_ptr())
+                        dx.data_ptr(), C, dw.data_ptr(), db.data_ptr(), part.data_ptr())
         _lib.check(lib.dta_ln_bwd(a, _lib.stream_handle(x2.device)))
         return dx.view(xshape), dw.to(wdt).view(wshape), db.to(bdt).view(bshape), None, None
 

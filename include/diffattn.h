@@ -114,6 +114,10 @@ typedef struct dta_attn_bwd_args {
                                 returned w.r.t. the UN-rotated projections -- the
                                 inverse rotation (apply_rotary_emb's backward) runs
                                 in the kernels' epilogues, no extra pass or buffer */
+  float* dcoef_partial;      /* optional fp32 workspace, dta_attn_bwd_dcoef_partial_bytes:
+                                with it dcoef is summed from per-wave partials in a fixed
+                                order (bitwise reproducible run to run); without it the
+                                query-major kernel adds into dcoef by float atomics */
 } dta_attn_bwd_args;
 
 enum { DTA_BWD_PRE = 1, DTA_BWD_DQ = 2, DTA_BWD_DKDV = 4 };
@@ -121,6 +125,7 @@ enum { DTA_BWD_PRE = 1, DTA_BWD_DQ = 2, DTA_BWD_DKDV = 4 };
 int dta_attn_bwd(const dta_attn_bwd_args* a, void* stream);
 size_t dta_attn_bwd_workspace_bytes(int32_t B, int32_t T, int32_t H, int32_t n_terms,
                                     int32_t head_size);
+size_t dta_attn_bwd_dcoef_partial_bytes(int32_t B, int32_t T, int32_t H, int32_t n_terms);
 
 /* Cross-head LayerNorm x out_scale (GroupLayerNorm.forward,
  * diff_transformer.py:15-20, then `out * (1 - self.lambda_init)`,
@@ -139,10 +144,14 @@ typedef struct dta_ln_args {
   const void* dy; int64_t dy_stride;
   void* dx; int64_t dx_stride;
   float* dw; float* db;              /* fp32 [C], accumulated (caller zeroes) */
+  float* partial;                    /* optional fp32 workspace (dta_ln_bwd_workspace_bytes):
+                                        per-block column partials summed in a fixed order, so
+                                        dw/db are bitwise reproducible; NULL: float atomics */
 } dta_ln_args;
 
 int dta_ln_fwd(const dta_ln_args* a, void* stream);
 int dta_ln_bwd(const dta_ln_args* a, void* stream);
+size_t dta_ln_bwd_workspace_bytes(int64_t rows, int64_t C);
 
 /* Interleaved-pair RoPE of every Q_i and K_i (apply_rotary_emb,
  * Ndiff_transformer.py:11-22 / control.py:11-22, rotation in fp32 then cast).

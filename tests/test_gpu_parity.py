@@ -273,3 +273,29 @@ def test_cfg2_full_shape_sampled_rows():
 def test_ndiff_long_sampled_rows():
     """N=4 at T=8192 (hs=64): the N-term plan over a long ring."""
     _long_case(B=1, H=2, N=4, hs=64, T=8192, pairs=[(0, 0), (0, 1)], n_rows=32, seed=5)
+
+
+def test_backward_reductions_are_reproducible():
+    """d(coef) (hence the lambda grads) and GroupLayerNorm dw/db are summed from
+    partials in a fixed order, not by float atomics: two backward passes over the
+    same inputs agree bitwise."""
+    ops = _ops()
+    H, N, hs, T, B = 4, 2, 64, 777, 2
+    g = torch.Generator().manual_seed(21)
+    W = ops.packed_width(H, N, hs, 2 * hs)
+    qkv = torch.randn(B, T, W, generator=g).to(torch.bfloat16).to(DEV)
+    coef = (torch.randn(H, N, generator=g) * 0.5).to(DEV)
+    do = torch.randn(B, T, H * 2 * hs, generator=g).to(torch.bfloat16).to(DEV)
+    w = (1 + 0.1 * torch.randn(1, 1, H * 2 * hs, generator=g)).to(DEV)
+    b = (0.1 * torch.randn(1, 1, H * 2 * hs, generator=g)).to(DEV)
+    grads = []
+    for _ in range(2):
+        xg = qkv.clone().requires_grad_(True)
+        cg = coef.clone().requires_grad_(True)
+        wg, bg = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+        out = ops.group_ln_scale(ops.diff_attention(xg, cg, H, N, hs), wg, bg, 1e-5, 0.2)
+        out.backward(do)
+        torch.cuda.synchronize()
+        grads.append([t.grad.clone() for t in (xg, cg, wg, bg)])
+    for a, b_ in zip(*grads):
+        assert torch.equal(a, b_)
