@@ -15,7 +15,7 @@ from torch.nn import functional as F
 
 from . import kv_cache, ops
 from .packing import ensure_packed, packed_linear
-from ._compat import (emit_tril_hooks, lambda_init_value, check_seq_len, check_dropout, fill_if_changed,
+from ._compat import (emit_tril_hooks, lambda_init_value, check_seq_len, attn_dropout_p, fill_if_changed,
                       mha_out_scale)
 from .diff_transformer import GroupLayerNorm, SwiGLU
 
@@ -97,14 +97,14 @@ class AlternatingDiffHead(nn.Module):
         self._check_terms()
         T = x.shape[1]
         check_seq_len(T, self.block_size)
-        check_dropout(self.dropout, self.training)
         init = lambda_init_value(layer_idx, self.lambda_init)
         fill_if_changed(self.lambda_init, init)
         coef = alternating_coefficients(torch.stack(list(self.lambda_qs)).float()[None],
                                         torch.stack(list(self.lambda_ks)).float()[None], init)
         qkv = F.linear(x, self.packed_weight())
         return ops.diff_attention(qkv, coef, 1, self.n_terms, self.head_size,
-                                  rope_table(self.freqs_cis, T, self.head_size))
+                                  rope_table(self.freqs_cis, T, self.head_size),
+                                  dropout_p=attn_dropout_p([self.dropout], self.training))
 
 
 class MultiHeadAlternatingDiffAttention(nn.Module):
@@ -148,12 +148,11 @@ class MultiHeadAlternatingDiffAttention(nn.Module):
         self.heads[0]._check_terms()
         T = x.shape[1]
         check_seq_len(T, self.block_size)
-        for h in self.heads:
-            check_dropout(h.dropout, self.training)
         coef = self.coefficients(layer_idx)
         qkv = packed_linear(x, self.packed_params(), self._pack)
         freqs = rope_table(self.heads[0].freqs_cis, T, self.head_size)
-        out = ops.diff_attention(qkv, coef, self.num_heads, self.n_terms, self.head_size, freqs)
+        out = ops.diff_attention(qkv, coef, self.num_heads, self.n_terms, self.head_size, freqs,
+                                 dropout_p=attn_dropout_p([h.dropout for h in self.heads], self.training))
         gn = self.group_norm
         out = ops.group_ln_scale(out, gn.weight, gn.bias, gn.eps, mha_out_scale(self.lambda_init))
         return self.dropout(self.proj(out))

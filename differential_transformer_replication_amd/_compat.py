@@ -95,8 +95,14 @@ def check_seq_len(T: int, block_size: int) -> None:
         raise RuntimeError(f"sequence length {T} exceeds block_size {block_size}")
 
 
-def check_dropout(drop: torch.nn.Dropout, training: bool) -> None:
-    if training and drop.p > 0:
-        raise NotImplementedError(
-            "attention-map dropout p > 0 is not implemented by the fused MI355X kernels; every "
-            "reference configuration uses dropout=0.0 (eval mode is unaffected)")
+def attn_dropout_p(drops, training: bool) -> float:
+    """The attention-map dropout probability the fused kernels apply: the heads'
+    nn.Dropout p in training (diff_transformer.py:66-67, Ndiff_transformer.py:114),
+    0 in eval.  All heads of one module share it (the reference builds them with the
+    same ``dropout``); differing per-head values are refused rather than ignored."""
+    if not training:
+        return 0.0
+    ps = {float(d.p) for d in drops}
+    if len(ps) != 1:
+        raise NotImplementedError("the fused kernels apply one attention-dropout p to every head of a module")
+    return ps.pop()

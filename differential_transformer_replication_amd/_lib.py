@@ -38,7 +38,8 @@ class AttnFwdArgs(ctypes.Structure):
                 ("H", ctypes.c_int32), ("n_terms", ctypes.c_int32), ("head_size", ctypes.c_int32),
                 ("dv", ctypes.c_int32), ("scale", ctypes.c_float), ("dropout_p", ctypes.c_float),
                 ("q", DtaTensor), ("k", DtaTensor), ("v", DtaTensor), ("o", DtaTensor),
-                ("obr", DtaTensor), ("lse", ctypes.c_void_p), ("coef", ctypes.c_void_p)]
+                ("obr", DtaTensor), ("lse", ctypes.c_void_p), ("coef", ctypes.c_void_p),
+                ("dropout_seed", ctypes.c_uint64)]
 
 
 class AttnBwdArgs(ctypes.Structure):
@@ -49,7 +50,8 @@ class AttnBwdArgs(ctypes.Structure):
                 ("lse", ctypes.c_void_p), ("coef", ctypes.c_void_p), ("dout", DtaTensor),
                 ("dq", DtaTensor), ("dk", DtaTensor), ("dv_out", DtaTensor),
                 ("dcoef", ctypes.c_void_p), ("delta", ctypes.c_void_p), ("dq_f32", ctypes.c_void_p),
-                ("stages", ctypes.c_int32), ("rope_freqs", ctypes.c_void_p), ("dcoef_partial", ctypes.c_void_p)]
+                ("stages", ctypes.c_int32), ("rope_freqs", ctypes.c_void_p), ("dcoef_partial", ctypes.c_void_p),
+                ("dropout_seed", ctypes.c_uint64)]
 
 
 BWD_PRE, BWD_DQ, BWD_DKDV = 1, 2, 4

@@ -4,11 +4,11 @@ attention with RoPE, the comparison baseline.
 The per-head projections are packed into one GEMM.  On the GPU the causal
 attention runs on the SAME fused gfx950 kernels as the differential models, as
 their N=1 case (one branch, coefficient 1, value width dv = hs; SURVEY 8(f) item
-2), so config 5 compares like with like.  Three cases keep PyTorch's
+2), so config 5 compares like with like -- attention-map dropout included (the
+kernels' counter-based mask, include/diffattn.h).  Two cases keep PyTorch's
 ``scaled_dot_product_attention`` instead: CPU tensors (the control model is not
-the hot path and stays runnable on the host), attention dropout p > 0 in
-training, which the fused kernels do not implement, and head sizes without a
-dv = hs plan (the fused plans cover 64 and 128).
+the hot path and stays runnable on the host) and head sizes without a dv = hs
+plan (the fused plans cover 64 and 128).
 """
 from __future__ import annotations
 
@@ -17,7 +17,7 @@ import torch.nn as nn
 from torch.nn import functional as F
 
 from . import kv_cache, ops
-from ._compat import emit_tril_hooks, check_seq_len
+from ._compat import emit_tril_hooks, check_seq_len, attn_dropout_p
 from .packing import ensure_packed, packed_linear
 from .Ndiff_transformer import precompute_freqs_cis, apply_rotary_emb, rope_table
 
@@ -29,15 +29,16 @@ def _fused_ok(x: torch.Tensor, p: float, hs: int) -> bool:
     # the fused kernels' standard-attention plans: head sizes 64 and 128 (dv = hs);
     # x.dtype is the projection's dtype under autocast too
     dt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else x.dtype
-    return x.is_cuda and p == 0.0 and ops.supported(dt, hs, 1, hs)
+    return x.is_cuda and 0.0 <= p < 1.0 and ops.supported(dt, hs, 1, hs)
 
 
-def _fused_attention(qkv: torch.Tensor, H: int, hs: int, freqs_cis: torch.Tensor) -> torch.Tensor:
+def _fused_attention(qkv: torch.Tensor, H: int, hs: int, freqs_cis: torch.Tensor, p: float = 0.0) -> torch.Tensor:
     """qkv (B, T, 3*H*hs) packed [Q | K | V] -> (B, T, H*hs): RoPE + causal softmax
-    attention (control.py:38-63) as the fused kernel's N=1, coef 1, dv=hs case."""
+    attention with map dropout p (control.py:38-63) as the fused kernel's N=1, coef 1,
+    dv=hs case."""
     T = qkv.shape[1]
     coef = torch.ones(H, 1, device=qkv.device, dtype=torch.float32)
-    return ops.diff_attention(qkv, coef, H, 1, hs, rope_table(freqs_cis, T, hs), dv=hs)
+    return ops.diff_attention(qkv, coef, H, 1, hs, rope_table(freqs_cis, T, hs), dv=hs, dropout_p=p)
 
 
 def _rope_fp32(x: torch.Tensor, freqs_cis: torch.Tensor) -> torch.Tensor:
@@ -66,11 +67,10 @@ class Head(nn.Module):
         p = self.dropout.p if self.training else 0.0
         if _fused_ok(x, p, self.head_size):
             w = torch.cat([self.query.weight, self.key.weight, self.value.weight], 0)
-            return _fused_attention(F.linear(x, w), 1, self.head_size, self.freqs_cis)
+            return _fused_attention(F.linear(x, w), 1, self.head_size, self.freqs_cis, p)
         q = _rope_fp32(self.query(x)[:, None], self.freqs_cis)
         k = _rope_fp32(self.key(x)[:, None], self.freqs_cis)
         v = self.value(x)[:, None]
-        p = self.dropout.p if self.training else 0.0
         out = F.scaled_dot_product_attention(q, k, v, is_causal=True, dropout_p=p,
                                              scale=1.0 / (self.head_size ** 0.5))
         return out[:, 0]
@@ -101,9 +101,9 @@ class MultiHeadAttention(nn.Module):
         H, hs = self.num_heads, self.head_size
         qkv = packed_linear(x, self.packed_params(), self._pack)
         fc = self.heads[0].freqs_cis
-        p = self.heads[0].dropout.p if self.training else 0.0
+        p = attn_dropout_p([h.dropout for h in self.heads], self.training)
         if _fused_ok(x, p, hs):
-            out = _fused_attention(qkv, H, hs, fc)
+            out = _fused_attention(qkv, H, hs, fc, p)
         else:
             q, k, v = qkv.view(B, T, 3, H, hs).permute(2, 0, 3, 1, 4)
             q, k = _rope_fp32(q, fc), _rope_fp32(k, fc)

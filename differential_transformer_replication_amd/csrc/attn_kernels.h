@@ -151,6 +151,23 @@ __device__ __forceinline__ void rope_inv4(const float* rope, int64_t row, int hs
   a0 = b0; a1 = b1; a2 = b2; a3 = b3;
 }
 
+// Attention dropout (nn.Dropout on every softmax map, diff_transformer.py:66-67,
+// Ndiff_transformer.py:114): element (q, k) of branch i of head h, batch b, is kept
+// iff hash(b, h, i, q, k, seed) >= p * 2^32, and kept elements are scaled by 1/(1-p).
+// The hash is counter-based (no state), so the forward and both backward kernels --
+// and the tests' torch restatement -- regenerate the same mask from the seed.
+__device__ __forceinline__ uint32_t fmix32(uint32_t x) {
+  x ^= x >> 16; x *= 0x85ebca6bu; x ^= x >> 13; x *= 0xc2b2ae35u; x ^= x >> 16;
+  return x;
+}
+__device__ __forceinline__ uint32_t drop_key(uint32_t seed_lo, uint32_t seed_hi, int b, int h, int i, int H, int N) {
+  return fmix32(seed_lo ^ fmix32((uint32_t)((b * H + h) * N + i) + seed_hi));
+}
+__device__ __forceinline__ float drop_mul(uint32_t key, int q, int k, uint32_t thr, float scale) {
+  const uint32_t x = fmix32((key + (uint32_t)q * 0x9e3779b1u) ^ ((uint32_t)k * 0x7feb352du));
+  return x >= thr ? scale : 0.f;
+}
+
 // ---- compile-time loops (asm immediates must be constants, not unrolled loop indices)
 template <class F, int... I>
 __device__ __forceinline__ void sfor_impl(F&& f, std::integer_sequence<int, I...>) {
@@ -462,7 +479,7 @@ struct FwdPick {
   static constexpr bool ok = FwdCfg<E, HS, N, DVC, NW, QREG>::bytes <= LIM;
 };
 
-template <class E, int HS, int N, int DVC, int NW, bool QREG, bool SRD>
+template <class E, int HS, int N, int DVC, int NW, bool QREG, bool SRD, bool DROP>
 __global__ __launch_bounds__(NW * 64, (FwdCfg<E, HS, N, DVC, NW, QREG>::WPE)) void attn_fwd_kernel(FwdParams p) {
   using O = Ops<E>;
   using frag = typename O::frag;
@@ -591,8 +608,9 @@ __global__ __launch_bounds__(NW * 64, (FwdCfg<E, HS, N, DVC, NW, QREG>::WPE)) vo
       }
     return fmaxf(a, b);
   };
-  // P = exp2(S * scale*log2e - m), row sums (two chains), packed to the PV operand
-  auto exp_pack = [&](int i, f32x16 (&sa)[NKB], frag (&pf)[NKB * SPB]) {
+  // P = exp2(S * scale*log2e - m), row sums (two chains), packed to the PV operand;
+  // with dropout the row sum keeps every element and the PV operand only the kept ones
+  auto exp_pack = [&](int i, int k0, f32x16 (&sa)[NKB], frag (&pf)[NKB * SPB]) {
     const float mi = m[i];
     float ls0 = 0.f, ls1 = 0.f;
 #pragma unroll
@@ -607,6 +625,14 @@ __global__ __launch_bounds__(NW * 64, (FwdCfg<E, HS, N, DVC, NW, QREG>::WPE)) vo
         ls1 += e1;
       }
     l[i] += ls0 + ls1;
+    if constexpr (DROP) {
+      const uint32_t key = drop_key(p.drop_seed_lo, p.drop_seed_hi, b, hh, i, p.H, N);
+#pragma unroll
+      for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          sa[kb][r] *= drop_mul(key, qrow, k0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hf, p.drop_thr, p.drop_scale);
+    }
 #pragma unroll
     for (int kb = 0; kb < NKB; ++kb) {
       if constexpr (SPB == 2) {
@@ -630,7 +656,7 @@ __global__ __launch_bounds__(NW * 64, (FwdCfg<E, HS, N, DVC, NW, QREG>::WPE)) vo
 #pragma unroll
       for (int d = 0; d < NDB; ++d) acc[i][d] *= alpha;
     }
-    exp_pack(i, sa, pf);
+    exp_pack(i, k0, sa, pf);
   };
   // QK^T + online softmax of one key tile for every branch, P packed as the PV B operand
   auto phase_a = [&](int kt, auto MASKED, frag (&pf)[N][NKB * SPB]) {
@@ -718,7 +744,7 @@ __global__ __launch_bounds__(NW * 64, (FwdCfg<E, HS, N, DVC, NW, QREG>::WPE)) vo
         }
       }
 #pragma unroll
-      for (int i = 0; i < N; ++i) exp_pack(i, sa[i], pf[i]);
+      for (int i = 0; i < N; ++i) exp_pack(i, k0, sa[i], pf[i]);
     }
   };
   // O_i^T += V^T P_i^T, one V fragment feeds every branch
@@ -1146,7 +1172,7 @@ struct DqPick {
   static constexpr bool ok = DqCfg<E, HS, N, DV, NW, QREG>::bytes <= LIM;
 };
 
-template <class E, int HS, int N, int DV, int NW, bool QREG, bool OUTF32, bool SRD>
+template <class E, int HS, int N, int DV, int NW, bool QREG, bool OUTF32, bool SRD, bool DROP>
 __global__ __launch_bounds__(NW * 64, simd_waves(NW, DqCfg<E, HS, N, DV, NW, QREG>::bytes))
 void attn_dq_kernel(BwdParams p) {
   using O = Ops<E>;
@@ -1362,13 +1388,19 @@ void attn_dq_kernel(BwdParams p) {
           // dS^T = c_i P^T (dP^T - delta_i) = P^T * (c_i dP^T - c_i delta_i)
           const float li = lse[i], ci = coef[i], cdi = coef[i] * del[i];
           const int lim = min(qrow, T - 1) - k0 - 4 * hf;
+          uint32_t dkey = 0;
+          if constexpr (DROP) dkey = drop_key(p.drop_seed_lo, p.drop_seed_hi, b, hh, i, p.H, N);
 #pragma unroll
           for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
               float arg = fmaf(sa[kb][r], p.sl2, li);      // li = -LSE
               if constexpr (MASK) arg = (kb * 32 + (r & 3) + 8 * (r >> 2) > lim) ? -INFINITY : arg;
-              sa[kb][r] = exp2_fast(arg) * fmaf(ci, dp[kb][r], -cdi);
+              // dropout: dA = c * mask/(1-p) * dP; dS = P (dA - c delta), delta from the dropped O_i
+              float cm = ci;
+              if constexpr (DROP)
+                cm *= drop_mul(dkey, qrow, k0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hf, p.drop_thr, p.drop_scale);
+              sa[kb][r] = exp2_fast(arg) * fmaf(cm, dp[kb][r], -cdi);
             }
           // dQ_i^T += K_i^T dS_i^T
           if constexpr (sizeof(E) == 2) {
@@ -1569,7 +1601,7 @@ struct DkdvWaves {
                          : DkdvCfg<E, HS, N, DV, 4>::bytes <= LIM ? 4 : 2;
 };
 
-template <class E, int HS, int N, int DV, int NW, bool DK, bool DVV, bool SRD>
+template <class E, int HS, int N, int DV, int NW, bool DK, bool DVV, bool SRD, bool DROP>
 __global__ __launch_bounds__(NW * 64, (NW >= 8 ? 2 : 1)) void attn_dkdv_kernel(BwdParams p) {
   using O = Ops<E>;
   using frag = typename O::frag;
@@ -1616,8 +1648,12 @@ __global__ __launch_bounds__(NW * 64, (NW >= 8 ? 2 : 1)) void attn_dkdv_kernel(B
   const int64_t bstride = (int64_t)p.B * p.H * T;
 
   float coef[N];
+  uint32_t dkey[N];
 #pragma unroll
-  for (int i = 0; i < N; ++i) coef[i] = p.coef[hh * N + i];
+  for (int i = 0; i < N; ++i) {
+    coef[i] = p.coef[hh * N + i];
+    dkey[i] = DROP ? drop_key(p.drop_seed_lo, p.drop_seed_hi, b, hh, i, p.H, N) : 0u;
+  }
   // this wave's key rows of every K_i and of V as B fragments
   // this wave's V rows as B fragments of dP = dO V^T (registers); K_i rows live in LDS
   frag vf[DK ? NSV : 1];
@@ -1746,8 +1782,10 @@ __global__ __launch_bounds__(NW * 64, (NW >= 8 ? 2 : 1)) void attn_dkdv_kernel(B
               arg = (rc < lim_lo || rc > lim_hi) ? -INFINITY : arg;
             }
             const float pr = exp2_fast(arg);
-            if constexpr (DVV) pc[r] = fmaf(coef[i], pr, pc[r]);
-            if constexpr (DK) sa[r] = pr * fmaf(coef[i], dpa[r], -d4[j]);
+            float cm = coef[i];                 // dropout: this map element's kept weight c_i * mask/(1-p)
+            if constexpr (DROP) cm *= drop_mul(dkey[i], q0 + (r & 3) + 8 * (r >> 2) + 4 * hf, krow, p.drop_thr, p.drop_scale);
+            if constexpr (DVV) pc[r] = fmaf(cm, pr, pc[r]);
+            if constexpr (DK) sa[r] = pr * fmaf(cm, dpa[r], -d4[j]);
           }
         }
         if constexpr (DK) {
@@ -2162,12 +2200,12 @@ inline bool fwd_pipe() {
   return on;
 }
 
-template <class E, int HS, int N, int DV_>
+template <class E, int HS, int N, int DV_, bool DROP>
 int launch_fwd_t(const FwdParams& p, hipStream_t st) {
   using PL = Plan<E, HS, N, DV_>;
   using FP = typename PL::FP;
   constexpr int DVC = FP::DVC, NW = FP::NW;
-  if constexpr (FwdPipeCfg<E, HS, N, DVC>::ok) {
+  if constexpr (!DROP && FwdPipeCfg<E, HS, N, DVC>::ok) {
     if (fwd_pipe() && kv_layout_ok(p, (int)sizeof(E))) {
       using PC = FwdPipeCfg<E, HS, N, DVC>;
       auto kern = attn_fwd_pipe_kernel<E, HS, N, DVC>;
@@ -2179,7 +2217,7 @@ int launch_fwd_t(const FwdParams& p, hipStream_t st) {
   constexpr int bytes = FwdCfg<E, HS, N, DVC, NW, FP::QREG>::bytes;
   dim3 grid((p.T + NW * 32 - 1) / (NW * 32), p.H * (PL::DV / DVC), p.B);
   auto run = [&](auto SRDV) -> int {
-    auto kern = attn_fwd_kernel<E, HS, N, DVC, NW, FP::QREG, decltype(SRDV)::value>;
+    auto kern = attn_fwd_kernel<E, HS, N, DVC, NW, FP::QREG, decltype(SRDV)::value, DROP>;
     if (int e = set_smem(kern, bytes)) return e;
     hipLaunchKernelGGL(kern, grid, dim3(NW * 64), bytes, st, p);
     return 0;
@@ -2193,7 +2231,7 @@ int launch_fwd_t(const FwdParams& p, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
-template <class E, int HS, int N, int DV_>
+template <class E, int HS, int N, int DV_, bool DROP>
 int launch_dq_t(const BwdParams& p, hipStream_t st) {
   using PL = Plan<E, HS, N, DV_>;
   constexpr int NW = PL::DP::NW, DV = PL::DV;
@@ -2201,7 +2239,7 @@ int launch_dq_t(const BwdParams& p, hipStream_t st) {
   constexpr int bytes = DqCfg<E, HS, N, DV, NW, QR>::bytes;
   dim3 grid((p.T + NW * 32 - 1) / (NW * 32), p.H, p.B);
   auto run = [&](auto F32, auto SRDV) -> int {
-    auto kern = attn_dq_kernel<E, HS, N, DV, NW, QR, decltype(F32)::value, decltype(SRDV)::value>;
+    auto kern = attn_dq_kernel<E, HS, N, DV, NW, QR, decltype(F32)::value, decltype(SRDV)::value, DROP>;
     if (int e = set_smem(kern, bytes)) return e;
     hipLaunchKernelGGL(kern, grid, dim3(NW * 64), bytes, st, p);
     return 0;
@@ -2216,11 +2254,11 @@ int launch_dq_t(const BwdParams& p, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
-template <class E, int HS, int N, int DV_>
+template <class E, int HS, int N, int DV_, bool DROP>
 int launch_dkdv_t(const BwdParams& p, hipStream_t st) {
   using PL = Plan<E, HS, N, DV_>;
   constexpr int NW = PL::KVW, DV = PL::DV;
-  if constexpr (Dkdv4Cfg<E, HS, N, DV>::ok) {
+  if constexpr (!DROP && Dkdv4Cfg<E, HS, N, DV>::ok) {
     if (dkdv_mode() == 4 && ring_layout_ok(p, (int)sizeof(E))) {
       using C4 = Dkdv4Cfg<E, HS, N, DV>;
       auto kern = attn_dkdv4_kernel<E, HS, N, DV>;
@@ -2234,7 +2272,8 @@ int launch_dkdv_t(const BwdParams& p, hipStream_t st) {
   dim3 block(NW * 64);
   constexpr bool FUSED = DkdvSplit<HS, N, DV>::fused;
   auto run = [&](auto DKV, auto DVVV, auto SRDV) -> int {
-    auto kern = attn_dkdv_kernel<E, HS, N, DV, NW, decltype(DKV)::value, decltype(DVVV)::value, decltype(SRDV)::value>;
+    auto kern = attn_dkdv_kernel<E, HS, N, DV, NW, decltype(DKV)::value, decltype(DVVV)::value, decltype(SRDV)::value,
+                                 DROP>;
     if (int e = set_smem(kern, bytes)) return e;
     hipLaunchKernelGGL(kern, grid, block, bytes, st, p);
     return 0;
@@ -2264,31 +2303,31 @@ int launch_dkdv_t(const BwdParams& p, hipStream_t st) {
   X(64, 1, 128) X(64, 2, 128) X(64, 3, 128) X(64, 4, 128) X(128, 1, 256) X(128, 2, 256) X(128, 3, 256) \
   X(128, 4, 256) X(64, 1, 64) X(128, 1, 128)
 
-template <class E>
+template <class E, bool DROP>
 int dispatch_fwd(const FwdParams& p, hipStream_t st) {
 #define DTA_F(HS_, N_, DV_) \
   if (p.HS == HS_ && p.N == N_ && p.DV == DV_) { \
-    if constexpr (Plan<E, HS_, N_, DV_>::ok) return launch_fwd_t<E, HS_, N_, DV_>(p, st); else return -2; }
+    if constexpr (Plan<E, HS_, N_, DV_>::ok) return launch_fwd_t<E, HS_, N_, DV_, DROP>(p, st); else return -2; }
   DTA_FOR_CONFIGS(DTA_F)
 #undef DTA_F
   return -2;
 }
 
-template <class E>
+template <class E, bool DROP>
 int dispatch_dq(const BwdParams& p, hipStream_t st) {
 #define DTA_Q(HS_, N_, DV_) \
   if (p.HS == HS_ && p.N == N_ && p.DV == DV_) { \
-    if constexpr (Plan<E, HS_, N_, DV_>::ok) return launch_dq_t<E, HS_, N_, DV_>(p, st); else return -2; }
+    if constexpr (Plan<E, HS_, N_, DV_>::ok) return launch_dq_t<E, HS_, N_, DV_, DROP>(p, st); else return -2; }
   DTA_FOR_CONFIGS(DTA_Q)
 #undef DTA_Q
   return -2;
 }
 
-template <class E>
+template <class E, bool DROP>
 int dispatch_dkdv(const BwdParams& p, hipStream_t st) {
 #define DTA_K(HS_, N_, DV_) \
   if (p.HS == HS_ && p.N == N_ && p.DV == DV_) { \
-    if constexpr (Plan<E, HS_, N_, DV_>::ok) return launch_dkdv_t<E, HS_, N_, DV_>(p, st); else return -2; }
+    if constexpr (Plan<E, HS_, N_, DV_>::ok) return launch_dkdv_t<E, HS_, N_, DV_, DROP>(p, st); else return -2; }
   DTA_FOR_CONFIGS(DTA_K)
 #undef DTA_K
   return -2;

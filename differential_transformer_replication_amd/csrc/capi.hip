@@ -14,11 +14,25 @@ int launch_attn_dq_f32(const BwdParams&, hipStream_t);
 int launch_attn_dkdv_bf16(const BwdParams&, hipStream_t);
 int launch_attn_dkdv_f16(const BwdParams&, hipStream_t);
 int launch_attn_dkdv_f32(const BwdParams&, hipStream_t);
+int launch_attn_fwd_bf16_drop(const FwdParams&, hipStream_t);
+int launch_attn_fwd_f16_drop(const FwdParams&, hipStream_t);
+int launch_attn_fwd_f32_drop(const FwdParams&, hipStream_t);
+int launch_attn_dq_bf16_drop(const BwdParams&, hipStream_t);
+int launch_attn_dq_f16_drop(const BwdParams&, hipStream_t);
+int launch_attn_dq_f32_drop(const BwdParams&, hipStream_t);
+int launch_attn_dkdv_bf16_drop(const BwdParams&, hipStream_t);
+int launch_attn_dkdv_f16_drop(const BwdParams&, hipStream_t);
+int launch_attn_dkdv_f32_drop(const BwdParams&, hipStream_t);
 bool attn_supported_bf16(int, int, int);
 bool attn_supported_f16(int, int, int);
 bool attn_supported_f32(int, int, int);
 
 int launch_attn_fwd(int dtype, const FwdParams& p, hipStream_t st) {
+  if (p.drop_thr) switch (dtype) {
+    case DTA_BF16: return launch_attn_fwd_bf16_drop(p, st);
+    case DTA_F16: return launch_attn_fwd_f16_drop(p, st);
+    case DTA_F32: return launch_attn_fwd_f32_drop(p, st);
+  }
   switch (dtype) {
     case DTA_BF16: return launch_attn_fwd_bf16(p, st);
     case DTA_F16: return launch_attn_fwd_f16(p, st);
@@ -27,6 +41,11 @@ int launch_attn_fwd(int dtype, const FwdParams& p, hipStream_t st) {
   return -2;
 }
 int launch_attn_dq(int dtype, const BwdParams& p, hipStream_t st) {
+  if (p.drop_thr) switch (dtype) {
+    case DTA_BF16: return launch_attn_dq_bf16_drop(p, st);
+    case DTA_F16: return launch_attn_dq_f16_drop(p, st);
+    case DTA_F32: return launch_attn_dq_f32_drop(p, st);
+  }
   switch (dtype) {
     case DTA_BF16: return launch_attn_dq_bf16(p, st);
     case DTA_F16: return launch_attn_dq_f16(p, st);
@@ -35,6 +54,11 @@ int launch_attn_dq(int dtype, const BwdParams& p, hipStream_t st) {
   return -2;
 }
 int launch_attn_dkdv(int dtype, const BwdParams& p, hipStream_t st) {
+  if (p.drop_thr) switch (dtype) {
+    case DTA_BF16: return launch_attn_dkdv_bf16_drop(p, st);
+    case DTA_F16: return launch_attn_dkdv_f16_drop(p, st);
+    case DTA_F32: return launch_attn_dkdv_f32_drop(p, st);
+  }
   switch (dtype) {
     case DTA_BF16: return launch_attn_dkdv_bf16(p, st);
     case DTA_F16: return launch_attn_dkdv_f16(p, st);
@@ -61,6 +85,17 @@ namespace {
 constexpr float kLog2e = 1.4426950408889634f;
 
 int esize(int dtype) { return dtype == DTA_F32 ? 4 : 2; }
+
+// attention dropout probability -> (keep threshold on a 32-bit hash, 1/(1-p)); p in [0, 1)
+bool drop_params(float p, uint64_t seed, uint32_t& thr, float& scale, uint32_t& lo, uint32_t& hi) {
+  if (!(p >= 0.f && p < 1.f)) return false;
+  const double t = (double)p * 4294967296.0;
+  thr = p > 0.f ? (uint32_t)(t < 1.0 ? 1.0 : (t > 4294967295.0 ? 4294967295.0 : t)) : 0u;
+  scale = p > 0.f ? (float)(1.0 / (1.0 - (double)p)) : 1.f;
+  lo = (uint32_t)seed;
+  hi = (uint32_t)(seed >> 32);
+  return true;
+}
 
 // element alignment every pointer/stride must have: one 16-byte vector
 int vec_elems(int dtype) { return 16 / esize(dtype); }
@@ -135,7 +170,7 @@ const char* dta_error_string(int code) {
     case DTA_ERR_INVALID: return "invalid argument (shape, null/misaligned pointer or stride)";
     case DTA_ERR_UNSUPPORTED: return "unsupported configuration (head_size/n_terms/dtype not built for gfx950)";
     case DTA_ERR_LAUNCH: return "HIP launch failed";
-    case DTA_ERR_DROPOUT: return "attention dropout p > 0 is not supported by the fused kernels";
+    case DTA_ERR_DROPOUT: return "attention dropout p must lie in [0, 1)";
   }
   return "unknown error";
 }
@@ -147,13 +182,14 @@ int dta_supported(int32_t dtype, int32_t head_size, int32_t n_terms, int32_t dv)
 int dta_attn_fwd(const dta_attn_fwd_args* a, void* stream) {
   if (!a) return DTA_ERR_INVALID;
   if (!ok_dims(a->dtype, a->B, a->T, a->H, a->n_terms, a->head_size, a->dv)) return DTA_ERR_INVALID;
-  if (a->dropout_p != 0.f) return DTA_ERR_DROPOUT;
+  FwdParams p{};
+  if (!drop_params(a->dropout_p, a->dropout_seed, p.drop_thr, p.drop_scale, p.drop_seed_lo, p.drop_seed_hi))
+    return DTA_ERR_DROPOUT;
   if (!attn_supported(a->dtype, a->head_size, a->n_terms, a->dv)) return DTA_ERR_UNSUPPORTED;
   if ((int64_t)a->B * a->T == 0) return DTA_OK;
   if (!ok_tensor(a->q, a->dtype, true) || !ok_tensor(a->k, a->dtype, true) || !ok_tensor(a->v, a->dtype, false) ||
       !ok_tensor(a->o, a->dtype, false) || !ok_tensor(a->obr, a->dtype, true) || !a->lse || !a->coef)
     return DTA_ERR_INVALID;
-  FwdParams p{};
   p.q = t5(a->q); p.k = t5(a->k); p.v = t5(a->v); p.o = t5(a->o); p.obr = t5(a->obr);
   p.lse = a->lse; p.coef = a->coef;
   p.B = a->B; p.T = a->T; p.H = a->H; p.N = a->n_terms; p.HS = a->head_size; p.DV = a->dv;
@@ -176,7 +212,9 @@ size_t dta_attn_bwd_workspace_bytes(int32_t B, int32_t T, int32_t H, int32_t n_t
 int dta_attn_bwd(const dta_attn_bwd_args* a, void* stream) {
   if (!a) return DTA_ERR_INVALID;
   if (!ok_dims(a->dtype, a->B, a->T, a->H, a->n_terms, a->head_size, a->dv)) return DTA_ERR_INVALID;
-  if (a->dropout_p != 0.f) return DTA_ERR_DROPOUT;
+  BwdParams p{};
+  if (!drop_params(a->dropout_p, a->dropout_seed, p.drop_thr, p.drop_scale, p.drop_seed_lo, p.drop_seed_hi))
+    return DTA_ERR_DROPOUT;
   if (!attn_supported(a->dtype, a->head_size, a->n_terms, a->dv)) return DTA_ERR_UNSUPPORTED;
   if (!a->dcoef) return DTA_ERR_INVALID;
   hipStream_t st = (hipStream_t)stream;
@@ -191,7 +229,6 @@ int dta_attn_bwd(const dta_attn_bwd_args* a, void* stream) {
       !a->lse || !a->coef || !a->delta)
     return DTA_ERR_INVALID;
   if (a->dq.ptr ? !ok_tensor(a->dq, a->dtype, true) : !aligned_ptr(a->dq_f32)) return DTA_ERR_INVALID;
-  BwdParams p{};
   p.q = t5(a->q); p.k = t5(a->k); p.v = t5(a->v); p.obr = t5(a->obr); p.dout = t5(a->dout);
   p.dq = t5(a->dq); p.dk = t5(a->dk); p.dv = t5(a->dv_out);
   p.lse = a->lse; p.delta = a->delta; p.coef = a->coef; p.dcoef = a->dcoef;

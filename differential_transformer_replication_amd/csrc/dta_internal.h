@@ -19,6 +19,9 @@ struct FwdParams {
   float sl2;           // scale * log2(e)
   int prio;            // 1: waves 4-7 of an 8-wave workgroup run at s_setprio 1
   unsigned long long* stamps;   // diagnostic builds (DTA_STAMPS) only: per-wave segment cycle sums
+  uint32_t drop_thr;   // attention dropout: keep iff hash >= drop_thr (= p * 2^32); 0 = off
+  float drop_scale;    // 1 / (1 - p)
+  uint32_t drop_seed_lo, drop_seed_hi;
 };
 
 struct BwdParams {
@@ -34,10 +37,17 @@ struct BwdParams {
   float sl2, scale;
   int prio;            // as FwdParams::prio
   unsigned long long* stamps;   // as FwdParams::stamps
+  uint32_t drop_thr;   // as FwdParams
+  float drop_scale;
+  uint32_t drop_seed_lo, drop_seed_hi;
 };
 
 // per-dtype launchers (dtype index: 0 bf16, 1 f16, 2 f32); return hipError_t
 int launch_attn_fwd(int dtype, const FwdParams& p, hipStream_t st);
+// dropout instantiations (attn_*_drop.hip): the same kernels with the mask compiled in
+int launch_attn_fwd_drop(int dtype, const FwdParams& p, hipStream_t st);
+int launch_attn_dq_drop(int dtype, const BwdParams& p, hipStream_t st);
+int launch_attn_dkdv_drop(int dtype, const BwdParams& p, hipStream_t st);
 int launch_attn_dq(int dtype, const BwdParams& p, hipStream_t st);
 int launch_attn_dkdv(int dtype, const BwdParams& p, hipStream_t st);
 bool attn_supported(int dtype, int hs, int n, int dv);

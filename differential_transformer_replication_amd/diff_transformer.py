@@ -17,7 +17,7 @@ from torch.nn import functional as F
 
 from . import kv_cache, ops
 from .packing import ensure_packed, packed_linear
-from ._compat import (emit_tril_hooks, lambda_init_value, check_seq_len, check_dropout, fill_if_changed,
+from ._compat import (emit_tril_hooks, lambda_init_value, check_seq_len, attn_dropout_p, fill_if_changed,
                       mha_out_scale)
 
 __all__ = ["GroupLayerNorm", "DiffHead", "MultiHeadDiffAttention", "SwiGLU", "Block", "DiffTransformer"]
@@ -83,13 +83,13 @@ class DiffHead(nn.Module):
 
     def forward(self, x, layer_idx):
         check_seq_len(x.shape[1], self.block_size)
-        check_dropout(self.dropout, self.training)
         init = lambda_init_value(layer_idx, self.lambda_init)
         fill_if_changed(self.lambda_init, init)
         coef = _layer_lambda_coef(self.lambda_q1[None].float(), self.lambda_k1[None].float(),
                                   self.lambda_q2[None].float(), self.lambda_k2[None].float(), init)
         qkv = F.linear(x, self.packed_weight())
-        return ops.diff_attention(qkv, coef, 1, 2, self.head_size)
+        return ops.diff_attention(qkv, coef, 1, 2, self.head_size,
+                                  dropout_p=attn_dropout_p([self.dropout], self.training))
 
 
 class MultiHeadDiffAttention(nn.Module):
@@ -128,11 +128,10 @@ class MultiHeadDiffAttention(nn.Module):
 
     def forward(self, x, layer_idx):
         check_seq_len(x.shape[1], self.block_size)
-        for h in self.heads:
-            check_dropout(h.dropout, self.training)
         coef = self.coefficients(layer_idx)
         qkv = packed_linear(x, self.packed_params(), self._pack)
-        out = ops.diff_attention(qkv, coef, self.num_heads, 2, self.head_size)
+        out = ops.diff_attention(qkv, coef, self.num_heads, 2, self.head_size,
+                                 dropout_p=attn_dropout_p([h.dropout for h in self.heads], self.training))
         # GroupLayerNorm then x(1 - lambda_init) with the MHA's own, never-updated 0.8 buffer
         gn = self.group_norm
         out = ops.group_ln_scale(out, gn.weight, gn.bias, gn.eps, mha_out_scale(self.lambda_init))

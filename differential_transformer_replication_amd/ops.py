@@ -90,7 +90,8 @@ def split_packed(qkv: Tensor, H: int, N: int, hs: int, dv: int):
 
 class _DiffAttention(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, qkv: Tensor, coef: Tensor, H: int, N: int, hs: int, freqs: Optional[Tensor], dv: int):
+    def forward(ctx, qkv: Tensor, coef: Tensor, H: int, N: int, hs: int, freqs: Optional[Tensor], dv: int,
+                dropout_p: float, seed: int):
         lib = _lib.load()
         _require_gpu(qkv, coef)
         if qkv.dim() != 3:
@@ -119,13 +120,14 @@ class _DiffAttention(torch.autograd.Function):
         obr = torch.empty(N, B, T, H, dv, device=dev, dtype=qkv.dtype)
         lse = torch.empty(N, B, H, T, device=dev, dtype=torch.float32)
         obr_t = _lib.DtaTensor(obr.data_ptr(), *obr.stride()[1:4], obr.stride(0))
-        a = _lib.AttnFwdArgs(dt, B, T, H, N, hs, dv, 1.0 / math.sqrt(hs), 0.0,
+        a = _lib.AttnFwdArgs(dt, B, T, H, N, hs, dv, 1.0 / math.sqrt(hs), dropout_p,
                              _lib.tensor5(q), _lib.tensor5(k), _lib.tensor5(v), _lib.tensor5(o), obr_t,
-                             lse.data_ptr(), coef.data_ptr())
+                             lse.data_ptr(), coef.data_ptr(), seed)
         with TIMER.region("attn_fwd"):
             _lib.check(lib.dta_attn_fwd(a, stream))
         ctx.save_for_backward(qkv, qk_rot, obr, lse, coef, freqs)
         ctx.dims = (H, N, hs, dv)
+        ctx.drop = (dropout_p, seed)
         return o.view(B, T, H * dv)
 
     @staticmethod
@@ -150,12 +152,12 @@ class _DiffAttention(torch.autograd.Function):
         # with RoPE the kernels differentiate w.r.t. the rotated Q/K (qk_rot) and their
         # dQ / dK epilogues apply the inverse rotation, writing straight into dqkv
         obr_t = _lib.DtaTensor(obr.data_ptr(), *obr.stride()[1:4], obr.stride(0))
-        a = _lib.AttnBwdArgs(dt, B, T, H, N, hs, dv, 1.0 / math.sqrt(hs), 0.0,
+        a = _lib.AttnBwdArgs(dt, B, T, H, N, hs, dv, 1.0 / math.sqrt(hs), ctx.drop[0],
                              _lib.tensor5(q), _lib.tensor5(k), _lib.tensor5(v), obr_t,
                              lse.data_ptr(), coef.data_ptr(), _lib.tensor5(do),
                              _lib.tensor5(dq), _lib.tensor5(dk), _lib.tensor5(dvv),
                              dcoef.data_ptr(), delta.data_ptr(), None, _lib.BWD_PRE,
-                             freqs.data_ptr() if freqs is not None else None, dcp.data_ptr())
+                             freqs.data_ptr() if freqs is not None else None, dcp.data_ptr(), ctx.drop[1])
         _lib.check(lib.dta_attn_bwd(a, stream))
         a.stages = _lib.BWD_DQ
         with TIMER.region("attn_bwd_dq"):
@@ -163,20 +165,30 @@ class _DiffAttention(torch.autograd.Function):
         a.stages = _lib.BWD_DKDV
         with TIMER.region("attn_bwd_dkdv"):
             _lib.check(lib.dta_attn_bwd(a, stream))
-        return dqkv, dcoef, None, None, None, None, None
+        return dqkv, dcoef, None, None, None, None, None, None, None
 
 
 def diff_attention(qkv: Tensor, coef: Tensor, H: int, N: int, hs: int,
-                   freqs: Optional[Tensor] = None, dv: Optional[int] = None) -> Tensor:
-    """O = sum_i coef[h,i] softmax_causal(Q_i K_i^T/sqrt(hs)) V for every head.
+                   freqs: Optional[Tensor] = None, dv: Optional[int] = None, dropout_p: float = 0.0,
+                   seed: Optional[int] = None) -> Tensor:
+    """O = sum_i coef[h,i] dropout(softmax_causal(Q_i K_i^T/sqrt(hs))) V for every head.
 
     ``freqs``: fp32 (T, hs/2, 2) rotary table (view_as_real of freqs_cis[:T]) or None.
     ``dv``: value width per head; 2*hs for the differential models (default), hs for
     standard attention (N=1, coef 1: control.py:38-63).
+    ``dropout_p``: nn.Dropout on every attention map (diff_transformer.py:66-67): each
+    map element kept with probability 1-p and scaled by 1/(1-p), independently per map,
+    from a counter-based hash of ``seed`` (include/diffattn.h); by default the seed is
+    drawn from torch's generator, so ``torch.manual_seed`` makes runs repeatable.
     """
     if freqs is not None:
         freqs = freqs.to(device=qkv.device, dtype=torch.float32).contiguous()
-    return _DiffAttention.apply(qkv, coef, H, N, hs, freqs, 2 * hs if dv is None else dv)
+    dropout_p = float(dropout_p)
+    if not 0.0 <= dropout_p < 1.0:
+        raise ValueError(f"dropout probability has to be in [0, 1), got {dropout_p}")
+    if seed is None:
+        seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if dropout_p > 0 else 0
+    return _DiffAttention.apply(qkv, coef, H, N, hs, freqs, 2 * hs if dv is None else dv, dropout_p, int(seed))
 
 
 class _GroupLNScale(torch.autograd.Function):

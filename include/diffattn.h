@@ -50,7 +50,7 @@ enum dta_status {
   DTA_ERR_INVALID = -1,      /* bad shape / stride / pointer / argument   */
   DTA_ERR_UNSUPPORTED = -2,  /* head_size / n_terms / dtype not built     */
   DTA_ERR_LAUNCH = -3,       /* hipLaunch / hipMemsetAsync failed         */
-  DTA_ERR_DROPOUT = -4       /* attention dropout p > 0 is not supported  */
+  DTA_ERR_DROPOUT = -4       /* attention dropout p outside [0, 1)         */
 };
 
 typedef struct dta_tensor {
@@ -68,12 +68,18 @@ typedef struct dta_attn_fwd_args {
   int32_t dtype;             /* enum dta_dtype */
   int32_t B, T, H, n_terms, head_size, dv;
   float scale;               /* 1/sqrt(head_size) (diff_transformer.py:57) */
-  float dropout_p;           /* must be 0 */
+  float dropout_p;           /* attention-map dropout in [0, 1) (diff_transformer.py:66-67):
+                                element (q, k) of map i of head h, batch b is kept iff
+                                fmix32((key + q*0x9e3779b1) ^ (k*0x7feb352d)) >= p*2^32,
+                                key = fmix32(seed_lo ^ fmix32(((b*H + h)*N + i) + seed_hi))
+                                (fmix32: murmur3's finaliser), kept elements x 1/(1-p);
+                                the row sums normalising the map see every element */
   dta_tensor q, k, v;        /* inputs */
   dta_tensor o;              /* output, combined */
   dta_tensor obr;            /* output [i][b][t][h][e]: sb,st,sh,si = strides of b,t,h,i */
   float* lse;                /* output fp32 [i][b][h][t], contiguous */
   const float* coef;         /* fp32 [h][i], contiguous */
+  uint64_t dropout_seed;     /* with dropout_p > 0: the mask's seed (pass the same to dta_attn_bwd) */
 } dta_attn_fwd_args;
 
 int dta_attn_fwd(const dta_attn_fwd_args* a, void* stream);
@@ -94,7 +100,7 @@ typedef struct dta_attn_bwd_args {
   int32_t dtype;
   int32_t B, T, H, n_terms, head_size, dv;
   float scale;
-  float dropout_p;
+  float dropout_p;           /* as dta_attn_fwd_args; obr must be the forward's (dropped) O_i */
   dta_tensor q, k, v, obr;
   const float* lse;          /* fp32 [i][b][h][t] from the forward */
   const float* coef;         /* fp32 [h][i] */
@@ -118,6 +124,7 @@ typedef struct dta_attn_bwd_args {
                                 with it dcoef is summed from per-wave partials in a fixed
                                 order (bitwise reproducible run to run); without it the
                                 query-major kernel adds into dcoef by float atomics */
+  uint64_t dropout_seed;     /* the forward's dropout seed */
 } dta_attn_bwd_args;
 
 enum { DTA_BWD_PRE = 1, DTA_BWD_DQ = 2, DTA_BWD_DKDV = 4 };

@@ -44,10 +44,11 @@ def test_invalid_args_rejected_without_gpu():
     lib = _lib.load()
     a = _lib.AttnFwdArgs()
     a.dtype, a.B, a.T, a.H, a.n_terms, a.head_size, a.dv = 0, 1, 8, 1, 2, 64, 128
+    a.dropout_p = 1.0
+    assert lib.dta_attn_fwd(a, None) == -4            # dropout p outside [0, 1) refused
     a.dropout_p = 0.5
-    assert lib.dta_attn_fwd(a, None) == -4            # dropout refused
+    assert lib.dta_attn_fwd(a, None) == -1            # null pointers refused (p = 0.5 itself is fine)
     a.dropout_p = 0.0
-    assert lib.dta_attn_fwd(a, None) == -1            # null pointers refused
     a.head_size, a.dv = 48, 96
     assert lib.dta_attn_fwd(a, None) == -2
     assert lib.dta_attn_fwd(None, None) == -1
@@ -170,6 +171,7 @@ def test_reference_errors_preserved():
     with pytest.raises(RuntimeError):
         ND.AlternatingDiffHead(16, 32, 0.0, 8, 0)(torch.randn(1, 4, 32), 1)   # n_terms = 0
     h = D.MultiHeadDiffAttention(2, 16, 64, 0.1, 8).train()
+    h.heads[1].dropout.p = 0.2                         # per-head p that differ: refused, not ignored
     with pytest.raises(NotImplementedError):
         h(torch.randn(1, 4, 64), 1)
 
