@@ -9,5 +9,5 @@ mkdir -p $C/build_v
 /opt/rocm/bin/hipcc $FLAGS $EXTRA -c ${SRC:-$C/attn_bf16.hip} -o $C/build_v/attn_bf16_$NAME.o
 /opt/rocm/bin/hipcc $FLAGS $EXTRA -c $C/capi.hip -o $C/build_v/capi_$NAME.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $C/build_v/capi_$NAME.o $C/build/elementwise.o $C/build/decode.o \
-  $C/build/attn_f16.o $C/build/attn_f32.o $C/build_v/attn_bf16_$NAME.o -o $C/../lib/libdiffattn_$NAME.so
+  $C/build/attn_f16.o $C/build/attn_f32.o $C/build/attn_bf16_drop.o $C/build/attn_f16_drop.o $C/build/attn_f32_drop.o $C/build_v/attn_bf16_$NAME.o -o $C/../lib/libdiffattn_$NAME.so
 echo built lib/libdiffattn_$NAME.so
