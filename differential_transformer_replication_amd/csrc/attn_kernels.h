@@ -40,6 +40,26 @@
 #define DTA_DQ_AHEAD 0
 #endif
 // dK/dV kernel: per-lane DMA source offsets computed once instead of per query tile
+// Measured-and-rejected schedule switches (cfg2 bf16, one-process A/B, tools/ab_kernels.py;
+// medians base -> variant, DESIGN.md "Experiments"):
+//   DTA_DKDV_STAGGER  waves 4-7 defer their dV product by one step   dK/dV 1.547 -> 1.747 ms (8 VGPR spill)
+//   DTA_FWD_LATE / DTA_DKDV_LATE   next tile's DMA after the compute  fwd 1.038 -> 1.035, dK/dV 1.564 -> 1.554 (noise)
+//   DTA_FWD_SPLIT / DTA_DKDV_SPLIT DMA slots spread over the step     fwd 1.010 -> 1.048, dK/dV 1.541 -> 1.616
+#ifndef DTA_DKDV_STAGGER
+#define DTA_DKDV_STAGGER 0
+#endif
+#ifndef DTA_FWD_LATE
+#define DTA_FWD_LATE 0
+#endif
+#ifndef DTA_DKDV_LATE
+#define DTA_DKDV_LATE 0
+#endif
+#ifndef DTA_FWD_SPLIT
+#define DTA_FWD_SPLIT 0
+#endif
+#ifndef DTA_DKDV_SPLIT
+#define DTA_DKDV_SPLIT 0
+#endif
 #ifndef DTA_DKDV_PREOFF
 #define DTA_DKDV_PREOFF 0
 #endif
@@ -373,6 +393,8 @@ struct KvRing {
     const int r = pb / VI::ROWB, c = ((pb % VI::ROWB) >> 4) ^ swz<VI::ROWB>(r);
     return (uint32_t)(r * (uint32_t)(st * ES) + c * 16);
   }
+  // slots [UA, UB) of this wave's pieces (the whole tile by default)
+  template <int UA = 0, int UB = MYP>
   __device__ static void issue(const E* gk, int64_t kst, int64_t ksi, const E* gv, int64_t vst, int k0, int T,
                                E* kdst, E* vdst, int wave, int lane) {
     const int rows = max(0, T - k0);           // a tile past T reads (as zeros) nothing
@@ -381,8 +403,8 @@ struct KvRing {
     const uint32_t nk = (uint32_t)rows * (uint32_t)(kst * ES), nv = (uint32_t)rows * (uint32_t)(vst * ES);
     char* kd = reinterpret_cast<char*>(kdst);
     char* vd = reinterpret_cast<char*>(vdst);
-    sfor<MYP>([&](auto U) {
-      constexpr int u = decltype(U)::value;
+    sfor<(UB > UA ? UB - UA : 0)>([&](auto U) {
+      constexpr int u = UA + decltype(U)::value;
       const int j = u * NW + wave;
       if constexpr ((u + 1) * NW <= PK) {
         buf_lds16(bk, nk, kd + j * 1024, offk(kst, ksi, j, lane));
@@ -554,6 +576,22 @@ __global__ __launch_bounds__(NW * 64, (FwdCfg<E, HS, N, DVC, NW, QREG>::WPE)) vo
   };
   const int tile_pieces = SRD ? KR::pieces(wave)
                               : N * stage_pieces<E, HS, BN, HS, NW>(wave) + stage_pieces<E, DVC, BN, DVC, NW>(wave);
+  // DTA_FWD_SPLIT: a wave's DMA pieces for tile kt+NS-1 go out one slot at a time over
+  // the step (slot 0 after the barrier, slot i+1 after branch i's S chain, the rest
+  // before PV) instead of all at once, so the workgroup's pieces do not queue together
+  constexpr bool FSPLIT = DTA_FWD_SPLIT && SRD && !DTA_FWD_PINGPONG && KR::MYP >= 2;
+  int split_kt = 0;
+  bool split_iss = false;
+  auto issue_slots = [&](auto UA, auto UB) {
+    constexpr int a = decltype(UA)::value < KR::MYP ? decltype(UA)::value : KR::MYP;
+    constexpr int e = decltype(UB)::value < KR::MYP ? decltype(UB)::value : KR::MYP;
+    if constexpr (e > a) {
+      const int kn = split_kt + NS - 1, bn = kn % NS;
+      if (split_iss)
+        KR::template issue<a, e>(gk, p.k.st, p.k.si, gv, p.v.st, kn * BN, T, Kb + bn * N * BN * HS,
+                                 Vb + bn * BN * DVC, wave, lane);
+    }
+  };
   // Ping-pong (PP): the two waves sharing a SIMD (w and w+4) run half a tile apart --
   // one in its QK^T + softmax phase (A) while the other is in its PV phase (B) -- so
   // the VALU-heavy half of one overlaps the MFMA-only half of the other instead of
@@ -719,6 +757,11 @@ __global__ __launch_bounds__(NW * 64, (FwdCfg<E, HS, N, DVC, NW, QREG>::WPE)) vo
           }
         }
       }
+      if constexpr (FSPLIT) {
+        if (i == 0) issue_slots(std::integral_constant<int, 1>{}, std::integral_constant<int, 2>{});
+        else if (i == 1) issue_slots(std::integral_constant<int, 2>{}, std::integral_constant<int, 3>{});
+        else if (i == 2) issue_slots(std::integral_constant<int, 3>{}, std::integral_constant<int, 4>{});
+      }
       if constexpr (!DTA_FWD_QKFIRST) softmax_branch(i, k0, MASKED, sa[i], pf[i]);
     }
     if constexpr (DTA_FWD_QKFIRST) {
@@ -805,15 +848,26 @@ __global__ __launch_bounds__(NW * 64, (FwdCfg<E, HS, N, DVC, NW, QREG>::WPE)) vo
       if (!g1) wait_vm(0);                   // tile kt+1 (staged at A(kt))
       lds_barrier();
     } else {
-      if (kt + NS - 1 < ntiles) stage_kv(kt + NS - 1, (kt + NS - 1) % NS);
+      if constexpr (FSPLIT) {
+        split_kt = kt;
+        split_iss = kt + NS - 1 < ntiles;
+        issue_slots(std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{});
+        if (!live) issue_slots(std::integral_constant<int, 1>{}, std::integral_constant<int, KR::MYP>{});
+      } else if (!DTA_FWD_LATE && kt + NS - 1 < ntiles) {
+        stage_kv(kt + NS - 1, (kt + NS - 1) % NS);
+      }
       st.lap<0>();
       if (live) {
         frag pf[N][NKB * SPB];
         phase_a(kt, MASKED, pf);
+        if constexpr (FSPLIT) issue_slots(std::integral_constant<int, (N < 3 ? N : 3) + 1>{},
+                                          std::integral_constant<int, KR::MYP>{});
         st.lap<1>();
         phase_b(kt, pf);
         st.lap<2>();
       }
+      // DTA_FWD_LATE: the next tile's DMA goes out after the compute, beside the barrier wait
+      if constexpr (DTA_FWD_LATE && !FSPLIT) if (kt + NS - 1 < ntiles) stage_kv(kt + NS - 1, (kt + NS - 1) % NS);
       // tile kt+1 must have landed; younger tiles may stay in flight
       wait_vm(tile_pieces * max(0, min(NS - 2, ntiles - 2 - kt)));
       st.lap<3>();
@@ -875,6 +929,9 @@ __global__ __launch_bounds__(NW * 64, (FwdCfg<E, HS, N, DVC, NW, QREG>::WPE)) vo
 // ends with tile t+2 landed (K(t+2) feeds the next iteration's QK^T).
 #ifndef DTA_FWD_PIPE_BN
 #define DTA_FWD_PIPE_BN 32   // 64: 1.088-1.133 ms, 32: 1.195 ms vs 1.02 for the 8-wave kernel (cfg2 A/B)
+#endif
+#ifndef DTA_FWD_PIPE_SGB      // 5: 1.230 ms, 8: 1.225 ms vs 1.124 (pipe, BN 64) and 1.017 (8-wave kernel)
+#define DTA_FWD_PIPE_SGB 0
 #endif
 #ifndef DTA_FWD_PIPE_PINQ
 #define DTA_FWD_PIPE_PINQ 0
@@ -1091,6 +1148,16 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_pipe_kernel(FwdParams p) {
       });
     }
     if constexpr (HAS_NEXT) mask_max(kt + 1, MASKNEXT, sn);
+    // DTA_FWD_PIPE_SGB = v: ask the scheduler for one MFMA then up to v VALU, throughout
+    // the block (LDS reads two per group up front), instead of its own clustering
+    if constexpr (DTA_FWD_PIPE_SGB > 0) {
+      constexpr int MF = (HAS_NEXT ? N * NKB * NSQ : 0) + NDB * NKB * 2 * N;
+      sfor<MF>([&](auto) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, DTA_FWD_PIPE_SGB, 0);
+      });
+    }
     pin();
     st.lap<2>();
     wait_vm(pieces);                     // tile kt+2 landed; tile kt+3 may fly
@@ -1497,6 +1564,8 @@ struct TileRing {
   // gq / gdo: (b, h) bases; lse / delta: (b, h) row-vector bases of branch 0.
   // Wave w issues pieces j = u * NW + w; a slot u whose NW pieces are all of one
   // kind is resolved at compile time (no per-piece scalar branching).
+  // slots [UA, UB) of this wave's pieces (the whole tile by default)
+  template <int UA = 0, int UB = MYP>
   __device__ static void issue(const BwdParams& p, const E* gq, const E* gdo, const float* lse, const float* delta,
                                int64_t bstride, int q0, int T, char* st0, int wave, int lane) {
     const int rows = T - q0;                       // > 0 for every issued tile
@@ -1504,8 +1573,8 @@ struct TileRing {
     const E* bd = gdo + (int64_t)q0 * p.dout.st;
     const uint32_t nq = (uint32_t)rows * (uint32_t)(p.q.st * ES), nd = (uint32_t)rows * (uint32_t)(p.dout.st * ES);
     const uint32_t nl = (uint32_t)(((N - 1) * bstride + rows) * 4);
-    sfor<MYP>([&](auto U) {
-      constexpr int u = decltype(U)::value;
+    sfor<(UB > UA ? UB - UA : 0)>([&](auto U) {
+      constexpr int u = UA + decltype(U)::value;
       const int j = u * NW + wave;
       if constexpr ((u + 1) * NW <= PQ) {
         buf_lds16(bq, nq, st0 + j * 1024, offq(p, j, lane));
@@ -1576,7 +1645,10 @@ struct DkdvCfg {
   static constexpr int nQ = N * BQ * HSP;
   static constexpr int nD = BQ * DV;
   static constexpr int nK = N * BK * HS;                   // the workgroup's K_i rows (B of S_i)
-  static constexpr int NS = ring_stages(nK * (int)sizeof(E), (nQ + nD) * (int)sizeof(E) + 2 * NP * 4);
+  // the stagger (DTA_DKDV_STAGGER) holds one stage longer: take a fifth when it fits
+  static constexpr int NS0 = ring_stages(nK * (int)sizeof(E), (nQ + nD) * (int)sizeof(E) + 2 * NP * 4);
+  static constexpr int NS = (DTA_DKDV_STAGGER && NS0 == 4 &&
+                             nK * (int)sizeof(E) + 5 * ((nQ + nD) * (int)sizeof(E) + 2 * NP * 4) <= 160 * 1024) ? 5 : NS0;
   static constexpr int bytes = (nK + NS * nQ + NS * nD) * (int)sizeof(E) + NS * 2 * NP * 4;
 };
 
@@ -1695,11 +1767,48 @@ __global__ __launch_bounds__(NW * 64, (NW >= 8 ? 2 : 1)) void attn_dkdv_kernel(B
   const int tile_pieces = SRD ? RG::pieces(wave)
                               : N * stage_pieces<E, HSP, BQ, HS, NW>(wave) + stage_pieces<E, DV, BQ, DV, NW>(wave) +
                                     rows_pieces<N, BQ, NW>(wave) * (DK ? 2 : 1);
-  for (int j = 0; j < NS - 1; ++j)
+  // DTA_DKDV_STAGGER: waves 4-7 (the second wave on each SIMD) run their dV product
+  // of tile t at the start of step t+1, so the two waves sharing a SIMD are shifted
+  // by one MFMA block and one's softmax VALU meets the other's MFMAs instead of the
+  // pair running in lockstep (MI355X_MICROARCH.md, two waves per SIMD, item 9).
+  // Their dO tile t is still read in step t+1, so the ring prefetches one tile less
+  // far ahead (LA = NS - 2): the slot refilled in step t held tile t-2, released by
+  // every wave at the barrier closing step t-1.
+  constexpr bool STG = DTA_DKDV_STAGGER && NW == 8 && DVV && sizeof(E) == 2 && NS >= 3;
+  constexpr int LA = STG ? NS - 2 : NS - 1;
+  const bool g1 = STG && wave >= NW / 2;
+  for (int j = 0; j < LA; ++j)
     if (j < ntiles) stage_q(kb0 + j * BQ, j);
-  wait_vm(tile_pieces * max(0, min(NS - 1, ntiles) - 1));
+  wait_vm(tile_pieces * max(0, min(LA, ntiles) - 1));
   lds_barrier();
   const bool wave_keys = kw0 < T;
+  // dV += (sum_i c_i P_i)^T dO of one tile from its packed P sums
+  auto dv_update = [&](const frag& p0, const frag& p1, const E* Dc) {
+    if constexpr (DVV && sizeof(E) == 2) {
+      const unsigned db = lds_addr(Dc);
+      const int Ld = tr_lane<DI::ROWB>(lane);
+      constexpr int NP2 = NVB >= 2 ? 2 : 1;       // d-blocks per LDS read batch
+      sfor<NVB / NP2>([&](auto D2) {
+        constexpr int d0 = NP2 * decltype(D2)::value;
+        lds64 r[NP2][4];
+        sfor<NP2>([&](auto E2) {
+          constexpr int d = d0 + decltype(E2)::value;
+          tr_issue<DI::ROWB, 0>(r[decltype(E2)::value], db + (Ld ^ (64 * d)), db + (Ld ^ (64 * d + 32)));
+        });
+        lgkm_pin<NP2>(r);
+#pragma unroll
+        for (int e = 0; e < NP2; ++e) {
+          dv[d0 + e] = O::mma(tr_frag<E>(r[e], 0), p0, dv[d0 + e]);
+          dv[d0 + e] = O::mma(tr_frag<E>(r[e], 1), p1, dv[d0 + e]);
+        }
+      });
+    }
+  };
+  auto slot_d = [&](int t) {
+    return SRD ? reinterpret_cast<const E*>(ringb + (t % NS) * RG::SB + RG::OFF_D) : Db + (t % NS) * BQ * DV;
+  };
+  frag pv0 = O::zero(), pv1 = O::zero();         // STG: waves 4-7's deferred P sums
+  bool pv_has = false;
   // static priority for the second-dispatched half (MI355X_MICROARCH.md, two waves per SIMD, item 4)
   if (NW == 8 && p.prio && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
 
@@ -1716,9 +1825,33 @@ __global__ __launch_bounds__(NW * 64, (NW >= 8 ? 2 : 1)) void attn_dkdv_kernel(B
     krow = kw0 + c32;
     const int buf = t % NS;
     const int q0 = kb0 + t * BQ;
-    if (t + NS - 1 < ntiles) stage_q(q0 + (NS - 1) * BQ, (t + NS - 1) % NS);
+    if constexpr (STG) {
+      if (pv_has) {                               // (g1 only) last step's deferred dV
+        dv_update(pv0, pv1, slot_d(t - 1));
+        pv_has = false;
+      }
+    }
+    // DTA_DKDV_SPLIT: this wave's DMA pieces for tile t+NS-1 go out in three parts
+    // spread over the step (after the barrier, after branch 0's S chain, before dV)
+    // instead of all at once, so 8 waves do not queue their pieces together
+    constexpr bool SPLIT = DTA_DKDV_SPLIT && SRD && !DTA_DKDV_PREOFF && RG::MYP >= 2 && !STG;
+    const bool iss = t + LA < ntiles;
+    auto issue_part = [&](auto UA, auto UB) {
+      if (iss)
+        RG::template issue<decltype(UA)::value, decltype(UB)::value>(
+            p, gq, gdo, p.lse + rowvec, p.delta + rowvec, bstride, q0 + (NS - 1) * BQ, T,
+            ringb + ((t + NS - 1) % NS) * RG::SB, wave, lane);
+    };
+    using U0 = std::integral_constant<int, 0>;
+    using U1 = std::integral_constant<int, 1>;
+    using U2 = std::integral_constant<int, (SPLIT && RG::MYP >= 3) ? 2 : 1>;
+    using UM = std::integral_constant<int, RG::MYP>;
+    if constexpr (SPLIT) issue_part(U0{}, U1{});
+    else if (!DTA_DKDV_LATE && iss) stage_q(q0 + LA * BQ, (t + LA) % NS);
     st.lap<0>();
-    if (wave_keys && q0 + BQ - 1 >= kw0) {
+    const bool busy = wave_keys && q0 + BQ - 1 >= kw0;
+    if constexpr (SPLIT) if (!busy) issue_part(U1{}, UM{});
+    if (busy) {
       const char* sg = ringb + buf * RG::SB;
       const E* Qc = SRD ? reinterpret_cast<const E*>(sg) : Qb + buf * N * BQ * HSP;
       const E* Dc = SRD ? reinterpret_cast<const E*>(sg + RG::OFF_D) : Db + buf * BQ * DV;
@@ -1766,6 +1899,7 @@ __global__ __launch_bounds__(NW * 64, (NW >= 8 ? 2 : 1)) void attn_dkdv_kernel(B
           for (int s = 0; s < NSQ; ++s)
             sa = O::mma(QI::row(Qi, c32, s, hf), KI::row(Ks + i * BK * HS, wave * 32 + c32, s, hf), sa);
         }
+        if constexpr (SPLIT) if (i == 0) issue_part(U1{}, U2{});
         // sa[r] = S_i[q0 + rowof(r)][krow]; rows 4g..4g+3 of a lane are consecutive.
         // Gc holds c_i * delta_i (written by attn_dq): dS = P * (c_i dP - c_i delta_i)
 #pragma unroll
@@ -1813,7 +1947,16 @@ __global__ __launch_bounds__(NW * 64, (NW >= 8 ? 2 : 1)) void attn_dkdv_kernel(B
         }
       }
       st.lap<2>();
-      if constexpr (DVV) {
+      if constexpr (SPLIT) issue_part(U2{}, UM{});
+      if constexpr (STG) {
+        if (g1) {
+          pv0 = O::template pack<0>(pc);
+          pv1 = O::template pack<1>(pc);
+          pv_has = true;
+        } else {
+          dv_update(O::template pack<0>(pc), O::template pack<1>(pc), Dc);
+        }
+      } else if constexpr (DVV) {
         if constexpr (sizeof(E) == 2) {
           const unsigned db = lds_addr(Dc);
           const int Ld = tr_lane<DI::ROWB>(lane);
@@ -1842,8 +1985,10 @@ __global__ __launch_bounds__(NW * 64, (NW >= 8 ? 2 : 1)) void attn_dkdv_kernel(B
       }
       }
     }
+    // DTA_DKDV_LATE: the next tile's DMA goes out after the compute, beside the barrier wait
+    if constexpr (DTA_DKDV_LATE && !SPLIT) if (iss) stage_q(q0 + LA * BQ, (t + LA) % NS);
     st.lap<3>();
-    wait_vm(tile_pieces * max(0, min(NS - 2, ntiles - 2 - t)));
+    wait_vm(tile_pieces * max(0, min(LA - 1, ntiles - 2 - t)));
     st.lap<4>();
     lds_barrier();
     st.lap<5>();
@@ -1854,6 +1999,8 @@ __global__ __launch_bounds__(NW * 64, (NW >= 8 ? 2 : 1)) void attn_dkdv_kernel(B
   for (int t = 0; t < thead; ++t) step(t, std::true_type{});
   for (int t = thead; t < ttail; ++t) step(t, std::false_type{});
   for (int t = ttail; t < ntiles; ++t) step(t, std::true_type{});
+  if constexpr (STG)
+    if (pv_has) dv_update(pv0, pv1, slot_d(ntiles - 1));   // no DMA refills this slot any more
   st.flush(p.stamps, lin * NW + wave, lane);
 
   if (!wave_keys || krow >= T) return;
