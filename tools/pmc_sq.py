@@ -1,12 +1,29 @@
 """Average per-launch value of every collected counter, per attention kernel, from
-rocprofv3 --pmc output directories.  Usage: python tools/pmc_sq.py <dir> [<dir> ...]"""
+rocprofv3 --pmc output directories, plus derived issue metrics.
+
+    python tools/pmc_sq.py <dir> [<dir> ...] [--json out.json]
+
+Derived (per launch; 1024 SIMDs, GRBM_GUI_ACTIVE summed over the 8 XCDs):
+  valu_per_mfma   SQ_INSTS_VALU / SQ_INSTS_MFMA
+  mfma_busy_frac  SQ_VALU_MFMA_BUSY_CYCLES / 1024 / (GRBM_GUI_ACTIVE / 8)
+  wait_inst_frac  SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES   (issue stalls: dependency / pipe busy)
+  wait_any_frac   SQ_WAIT_ANY / SQ_WAVE_CYCLES        (parked in s_waitcnt / s_barrier)
+  active_frac     SQ_ACTIVE_INST_ANY / SQ_WAVE_CYCLES
+"""
 import csv
 import glob
+import json
 import sys
 from collections import defaultdict
 
+args = sys.argv[1:]
+out_json = None
+if "--json" in args:
+    i = args.index("--json")
+    out_json = args[i + 1]
+    args = args[:i] + args[i + 2:]
 vals = defaultdict(list)
-for d in sys.argv[1:]:
+for d in args:
     for f in glob.glob(d + "/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
             k = r["Kernel_Name"]
@@ -16,3 +33,24 @@ for d in sys.argv[1:]:
                 vals[(short, r["Counter_Name"])].append(float(r["Counter_Value"]))
 for (k, c), v in sorted(vals.items()):
     print(f"{k:12s} {c:32s} {sum(v) / len(v):16.1f}  (n={len(v)})")
+per = defaultdict(dict)
+for (k, c), v in vals.items():
+    per[k][c] = sum(v) / len(v)
+res = {}
+for k, c in sorted(per.items()):
+    d = {"counters": {n: round(x, 1) for n, x in sorted(c.items())}}
+    g = lambda n: c.get(n)
+    if g("SQ_INSTS_VALU") and g("SQ_INSTS_MFMA"):
+        d["valu_per_mfma"] = round(g("SQ_INSTS_VALU") / g("SQ_INSTS_MFMA"), 2)
+    if g("SQ_VALU_MFMA_BUSY_CYCLES") and g("GRBM_GUI_ACTIVE"):
+        d["mfma_busy_frac"] = round(g("SQ_VALU_MFMA_BUSY_CYCLES") / 1024 / (g("GRBM_GUI_ACTIVE") / 8), 4)
+    for name, num in (("wait_inst_frac", "SQ_WAIT_INST_ANY"), ("wait_any_frac", "SQ_WAIT_ANY"),
+                      ("active_frac", "SQ_ACTIVE_INST_ANY")):
+        if g(num) and g("SQ_WAVE_CYCLES"):
+            d[name] = round(g(num) / g("SQ_WAVE_CYCLES"), 4)
+    res[k] = d
+    print(k, {n: v for n, v in d.items() if n != "counters"})
+if out_json:
+    json.dump({"source": "rocprofv3 --pmc, one counter group per pass, python3 bench.py --cpu-baseline off "
+                         "--train-steps 0 --no-hbm --steps 2 --warmup 1 (tools/round_gpu.sh)",
+               "kernels": res}, open(out_json, "w"), indent=1)

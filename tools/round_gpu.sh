@@ -33,6 +33,6 @@ if [ -n "$SQ" ]; then
     i=$((i+1))
     timeout -s KILL 120 rocprofv3 --pmc $grp --output-format csv -d $OUT/sq$i -o run -- python3 $R/bench.py $PB --no-hbm --steps 2 --warmup 1 > $OUT/sq$i.log 2>&1 || { echo "SQ group $i failed"; tail -5 $OUT/sq$i.log; exit 1; }
   done
-  python3 $R/tools/pmc_sq.py $OUT/sq1 $OUT/sq2 > $OUT/sq_summary.txt && cat $OUT/sq_summary.txt
+  python3 $R/tools/pmc_sq.py $OUT/sq1 $OUT/sq2 --json $OUT/sq.json > $OUT/sq_summary.txt && cat $OUT/sq_summary.txt
 fi
 echo ROUND_GPU_OK
