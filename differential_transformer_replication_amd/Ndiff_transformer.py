@@ -14,7 +14,7 @@ import torch.nn as nn
 from torch.nn import functional as F
 
 from . import kv_cache, ops
-from .packing import ensure_packed, packed_linear
+from .packing import ensure_packed, packed_linear, packed_tensor
 from ._compat import (emit_tril_hooks, lambda_init_value, check_seq_len, attn_dropout_p, fill_if_changed,
                       mha_out_scale)
 from .diff_transformer import GroupLayerNorm, SwiGLU
@@ -123,6 +123,7 @@ class MultiHeadAlternatingDiffAttention(nn.Module):
         self.n_terms = n_terms
         self.block_size = block_size
         self._pack = {}                            # the shared storage of the heads' projections
+        self._lam_pack = {}                        # ... and of their lambda vectors
 
     def packed_params(self):
         """Every head's projection weights in the kernel's packed row order."""
@@ -139,10 +140,17 @@ class MultiHeadAlternatingDiffAttention(nn.Module):
         init = lambda_init_value(layer_idx, self.heads[0].lambda_init)
         for h in self.heads:
             fill_if_changed(h.lambda_init, init)
-        lqs = torch.stack([p for h in self.heads for p in h.lambda_qs]).float()
-        lks = torch.stack([p for h in self.heads for p in h.lambda_ks]).float()
-        shape = (self.num_heads, self.n_terms, self.head_size)
-        return alternating_coefficients(lqs.view(shape), lks.view(shape), init)
+        # the 2NH lambda vectors are row views of one pack: one copy forward, one add backward
+        lam = packed_tensor(self.lambda_params(), self._lam_pack).view(
+            2, self.num_heads, self.n_terms, self.head_size).float()
+        return alternating_coefficients(lam[0], lam[1], init)
+
+    def lambda_params(self):
+        return [p for h in self.heads for p in h.lambda_qs] + [p for h in self.heads for p in h.lambda_ks]
+
+    def param_packs(self):
+        """(holder, params) of every shared-storage parameter group (dp.BucketedAllReduce)."""
+        return [(self._pack, self.packed_params()), (self._lam_pack, self.lambda_params())]
 
     def forward(self, x, layer_idx):
         self.heads[0]._check_terms()
@@ -166,8 +174,8 @@ class Block(nn.Module):
         head_size = n_embd // (n_head * 2)
         self.diff_attn = MultiHeadAlternatingDiffAttention(n_head, head_size, n_embd, dropout, block_size, n_terms)
         self.ffwd = nn.Sequential(SwiGLU(n_embd, 4 * n_embd), nn.Linear(4 * n_embd, n_embd), nn.Dropout(dropout))
-        self.ln1 = nn.LayerNorm(n_embd)
-        self.ln2 = nn.LayerNorm(n_embd)
+        self.ln1 = ops.LayerNorm(n_embd)
+        self.ln2 = ops.LayerNorm(n_embd)
 
     def forward(self, x, layer_idx):
         x = x + self.diff_attn(self.ln1(x), layer_idx)
@@ -183,7 +191,7 @@ class AlternatingDiffTransformer(nn.Module):
         self.block_size = block_size
         self.token_embedding_table = nn.Embedding(vocab_size, n_embd)
         self.blocks = nn.ModuleList([Block(n_embd, n_head, block_size, dropout, n_terms) for _ in range(n_layer)])
-        self.ln_f = nn.LayerNorm(n_embd)
+        self.ln_f = ops.LayerNorm(n_embd)
         self.lm_head = nn.Linear(n_embd, vocab_size)
         self.apply(self._init_weights)
 

@@ -25,12 +25,22 @@ ABI_VERSION = 2
 EXPORTS = ("dta_attn_fwd", "dta_attn_bwd", "dta_attn_bwd_workspace_bytes", "dta_attn_bwd_dcoef_partial_bytes",
            "dta_ln_fwd", "dta_ln_bwd", "dta_ln_bwd_workspace_bytes",
            "dta_rope", "dta_cast_f32", "dta_error_string", "dta_abi_version", "dta_supported",
-           "dta_attn_decode", "dta_attn_decode_workspace_bytes")
+           "dta_attn_decode", "dta_attn_decode_workspace_bytes", "dta_swiglu_fwd", "dta_swiglu_bwd")
 
 
 class DtaTensor(ctypes.Structure):
     _fields_ = [("ptr", ctypes.c_void_p), ("sb", ctypes.c_int64), ("st", ctypes.c_int64),
                 ("sh", ctypes.c_int64), ("si", ctypes.c_int64)]
+
+
+class SwigluArgs(ctypes.Structure):
+    _fields_ = [("dtype", ctypes.c_int32), ("rows", ctypes.c_int64), ("n", ctypes.c_int64),
+                ("a", ctypes.c_void_p), ("a_stride", ctypes.c_int64),
+                ("b", ctypes.c_void_p), ("b_stride", ctypes.c_int64),
+                ("out", ctypes.c_void_p), ("out_stride", ctypes.c_int64),
+                ("dout", ctypes.c_void_p), ("dout_stride", ctypes.c_int64),
+                ("da", ctypes.c_void_p), ("da_stride", ctypes.c_int64),
+                ("db", ctypes.c_void_p), ("db_stride", ctypes.c_int64)]
 
 
 class AttnFwdArgs(ctypes.Structure):
@@ -104,6 +114,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         lib.dta_ln_fwd.argtypes = [P(LnArgs), ctypes.c_void_p]
         lib.dta_ln_bwd.argtypes = [P(LnArgs), ctypes.c_void_p]
         lib.dta_rope.argtypes = [P(RopeArgs), ctypes.c_void_p]
+        lib.dta_swiglu_fwd.argtypes = [P(SwigluArgs), ctypes.c_void_p]
+        lib.dta_swiglu_bwd.argtypes = [P(SwigluArgs), ctypes.c_void_p]
         lib.dta_cast_f32.argtypes = [ctypes.c_int32] * 6 + [ctypes.c_void_p, DtaTensor, ctypes.c_void_p]
         lib.dta_attn_decode.argtypes = [P(DecodeArgs), ctypes.c_void_p]
         lib.dta_attn_decode_workspace_bytes.argtypes = [ctypes.c_int32] * 6
@@ -118,7 +130,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         lib.dta_error_string.restype = ctypes.c_char_p
         lib.dta_supported.argtypes = [ctypes.c_int32] * 4
         for fn in ("dta_attn_fwd", "dta_attn_bwd", "dta_attn_decode", "dta_ln_fwd", "dta_ln_bwd", "dta_rope", "dta_cast_f32",
-                   "dta_abi_version", "dta_supported"):
+                   "dta_abi_version", "dta_supported", "dta_swiglu_fwd", "dta_swiglu_bwd"):
             getattr(lib, fn).restype = ctypes.c_int
         if lib.dta_abi_version() != ABI_VERSION:
             raise RuntimeError(f"libdiffattn ABI {lib.dta_abi_version()} != expected {ABI_VERSION}")

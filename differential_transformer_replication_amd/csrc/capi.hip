@@ -296,6 +296,31 @@ int dta_rope(const dta_rope_args* a, void* stream) {
   return status(launch_rope(a->dtype, a->src_f32 != 0, p, (hipStream_t)stream));
 }
 
+static int swiglu_common(const dta_swiglu_args* a, bool bwd, SwigluParams& p) {
+  if (!a || a->dtype < DTA_BF16 || a->dtype > DTA_F32 || a->rows < 0 || a->n < 0) return DTA_ERR_INVALID;
+  if (a->n % 8) return DTA_ERR_UNSUPPORTED;
+  auto ok = [](const void* q, int64_t st) { return aligned_ptr(q) && st % 8 == 0 && st >= 0; };
+  if (!ok(a->a, a->a_stride) || !ok(a->b, a->b_stride)) return DTA_ERR_INVALID;
+  if (!bwd && !ok(a->out, a->out_stride)) return DTA_ERR_INVALID;
+  if (bwd && (!ok(a->dout, a->dout_stride) || !ok(a->da, a->da_stride) || !ok(a->db, a->db_stride)))
+    return DTA_ERR_INVALID;
+  p = SwigluParams{a->rows, a->n, a->a, a->a_stride, a->b, a->b_stride, a->out, a->out_stride,
+                   a->dout, a->dout_stride, a->da, a->da_stride, a->db, a->db_stride};
+  return DTA_OK;
+}
+
+int dta_swiglu_fwd(const dta_swiglu_args* a, void* stream) {
+  SwigluParams p;
+  if (int e = swiglu_common(a, false, p)) return e;
+  return status(launch_swiglu(a->dtype, p, false, (hipStream_t)stream));
+}
+
+int dta_swiglu_bwd(const dta_swiglu_args* a, void* stream) {
+  SwigluParams p;
+  if (int e = swiglu_common(a, true, p)) return e;
+  return status(launch_swiglu(a->dtype, p, true, (hipStream_t)stream));
+}
+
 int dta_cast_f32(int32_t dtype, int32_t B, int32_t T, int32_t H, int32_t n_terms, int32_t head_size,
                  const float* src, dta_tensor dst, void* stream) {
   if (!ok_dims(dtype, B, T, H, n_terms, head_size, 1) || head_size % 8) return DTA_ERR_INVALID;

@@ -102,4 +102,15 @@ int launch_dcoef(const float* delta, float* dcoef, int B, int T, int H, int N, h
 int launch_dcoef_reduce(const float* part, float* dcoef, int H, int N, int64_t per, hipStream_t st);
 int launch_cast(int dtype, const float* src, const T5& dst, int B, int T, int H, int N, int HS, hipStream_t st);
 
+struct SwigluParams {
+  int64_t rows, n;                       // rows x n elements, n % 8 == 0
+  const void* a; int64_t as;             // gate pre-activation (row stride, elements)
+  const void* b; int64_t bs;             // linear branch
+  void* out; int64_t os;                 // forward output
+  const void* dout; int64_t dos;         // backward: incoming gradient
+  void* da; int64_t das;
+  void* db; int64_t dbs;
+};
+int launch_swiglu(int dtype, const SwigluParams& p, bool bwd, hipStream_t st);
+
 }  // namespace dta

@@ -9,6 +9,8 @@
 //  * bwd_delta         delta_i[b,h,t] = <dO, O_i> per row (flash-bwd preprocess);
 //  * dcoef_reduce      dcoef[h][i] = sum_{b,t} delta_i  (d lambda, SURVEY semantic 5).
 //  * cast_f32          fp32 dQ accumulator -> activation dtype.
+#include <type_traits>
+
 #include "dta_common.h"
 #include "dta_internal.h"
 
@@ -218,6 +220,128 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnParams p) {
   }
 }
 
+// Backward, one workgroup per row at a time (DTA_LN_BWD_ROWBLOCK, default): the four
+// waves split the row's columns (thread t owns 8-column chunks t, t+256, ...), so a
+// thread's dw/db column partials are only 16*CHB registers and need no cross-wave
+// reduction; the row sums (sum g, sum g*xhat) cross waves through a parity-double-
+// buffered LDS slot, one barrier per row.  The next row's x / dy are loaded before
+// the current row's math.  ~60 VGPRs: 4 workgroups (16 waves) per CU, where the
+// wave-per-row kernel above holds 222 registers for C = 2048 (8 waves per CU).
+template <class E, int CHB>
+__global__ __launch_bounds__(256) void ln_bwd_rb_kernel(LnParams p) {
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  float dwp[CHB][8], dbp[CHB][8];
+#pragma unroll
+  for (int c = 0; c < CHB; ++c)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { dwp[c][j] = 0.f; dbp[c][j] = 0.f; }
+  const float inv_c = 1.f / (float)p.C;
+  __shared__ float red[2][4][2];
+  constexpr bool P16 = sizeof(E) == 2;
+  typedef typename std::conditional<P16, s16x8, f32x4>::type RT;
+  constexpr int NR = P16 ? 1 : 2;                        // raw vectors per 8 elements
+  RT xr[2][CHB][NR], dr[2][CHB][NR];
+  auto load = [&](auto S, int64_t r) {
+    constexpr int s = decltype(S)::value;
+    const E* x = reinterpret_cast<const E*>(p.x) + r * p.xs;
+    const E* dy = reinterpret_cast<const E*>(p.dy) + r * p.dys;
+#pragma unroll
+    for (int c = 0; c < CHB; ++c) {
+      const int col = (c * 256 + t) * 8;
+      if (col < p.C) {
+#pragma unroll
+        for (int k = 0; k < NR; ++k) {
+          xr[s][c][k] = *reinterpret_cast<const RT*>(x + col + k * 4);
+          dr[s][c][k] = *reinterpret_cast<const RT*>(dy + col + k * 4);
+        }
+      }
+    }
+  };
+  auto cvt = [&](const RT (&v)[NR], float* f) {
+    if constexpr (P16) {
+      raw_cvt<E>(v[0], f);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { f[j] = v[0][j]; f[j + 4] = v[1][j]; }
+    }
+  };
+  const int64_t stride = gridDim.x;
+  int par = 0;
+  auto body = [&](auto S, int64_t r) {
+    constexpr int s = decltype(S)::value;
+    if (r + stride < p.rows) load(std::integral_constant<int, 1 - s>{}, r + stride);   // next row in flight
+    const float mean = p.mean[r], rstd = p.rstd[r];
+    float xh[CHB][8], g[CHB][8];
+    float sg = 0.f, sgx = 0.f;
+#pragma unroll
+    for (int c = 0; c < CHB; ++c) {
+      const int col = (c * 256 + t) * 8;
+      if (col < p.C) {
+        float xv[8], dv[8];
+        cvt(xr[s][c], xv);
+        cvt(dr[s][c], dv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          xh[c][j] = (xv[j] - mean) * rstd;
+          const float dys = dv[j] * p.out_scale;
+          dwp[c][j] = fmaf(dys, xh[c][j], dwp[c][j]);
+          dbp[c][j] += dys;
+          g[c][j] = dys * p.w[col + j];
+          sg += g[c][j];
+          sgx = fmaf(g[c][j], xh[c][j], sgx);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { xh[c][j] = 0.f; g[c][j] = 0.f; }
+      }
+    }
+    sg = wave_sum(sg);
+    sgx = wave_sum(sgx);
+    if (lane == 0) { red[par][wave][0] = sg; red[par][wave][1] = sgx; }
+    __syncthreads();
+    const float mg = (red[par][0][0] + red[par][1][0] + red[par][2][0] + red[par][3][0]) * inv_c;
+    const float mgx = (red[par][0][1] + red[par][1][1] + red[par][2][1] + red[par][3][1]) * inv_c;
+    par ^= 1;
+    E* dx = reinterpret_cast<E*>(p.dx) + r * p.dxs;
+#pragma unroll
+    for (int c = 0; c < CHB; ++c) {
+      const int col = (c * 256 + t) * 8;
+      if (col < p.C) {
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = rstd * (g[c][j] - mg - xh[c][j] * mgx);
+        st8<E>(dx + col, o);
+      }
+    }
+  };
+  int64_t r = blockIdx.x;
+  if (r < p.rows) load(std::integral_constant<int, 0>{}, r);
+  while (r < p.rows) {
+    body(std::integral_constant<int, 0>{}, r);
+    r += stride;
+    if (r >= p.rows) break;
+    body(std::integral_constant<int, 1>{}, r);
+    r += stride;
+  }
+#pragma unroll
+  for (int c = 0; c < CHB; ++c) {
+    const int col = (c * 256 + t) * 8;
+    if (col < p.C) {
+      if (p.partial) {
+        float* pw = p.partial + ((int64_t)blockIdx.x * 2) * p.C + col;
+        float* pb = pw + p.C;
+        *reinterpret_cast<f32x4*>(pw) = f32x4{dwp[c][0], dwp[c][1], dwp[c][2], dwp[c][3]};
+        *reinterpret_cast<f32x4*>(pw + 4) = f32x4{dwp[c][4], dwp[c][5], dwp[c][6], dwp[c][7]};
+        *reinterpret_cast<f32x4*>(pb) = f32x4{dbp[c][0], dbp[c][1], dbp[c][2], dbp[c][3]};
+        *reinterpret_cast<f32x4*>(pb + 4) = f32x4{dbp[c][4], dbp[c][5], dbp[c][6], dbp[c][7]};
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { atomicAdd(p.dw + col + j, dwp[c][j]); atomicAdd(p.db + col + j, dbp[c][j]); }
+      }
+    }
+  }
+}
+
 // dw / db += the column sums of the per-block partials, in a fixed order: pass 1 sums
 // each of kLnChunks contiguous runs of blocks per column (many threads in flight),
 // pass 2 adds the kLnChunks run sums in order
@@ -339,6 +463,9 @@ static inline int grid_for(int64_t items) {
   return (int)(g > 16384 ? 16384 : (g < 1 ? 1 : g));
 }
 
+#ifndef DTA_LN_BWD_ROWBLOCK
+#define DTA_LN_BWD_ROWBLOCK 1
+#endif
 // blocks of the LN backward: enough waves in flight to cover HBM latency, few enough
 // that the per-block column partials stay small (dta_ln_bwd_workspace_bytes)
 int ln_bwd_blocks(int64_t rows) { return (int)std::min<int64_t>((rows + 7) / 8, 1024); }
@@ -352,7 +479,10 @@ int ln_launch(const LnParams& p, bool bwd, hipStream_t st) {
 #define DTA_LN(CH_)                                                                    \
   if (ch <= CH_) {                                                                     \
     if (bwd) {                                                                         \
-      hipLaunchKernelGGL((ln_bwd_kernel<E, CH_>), dim3(bwd_grid), dim3(256), 0, st, p); \
+      if (DTA_LN_BWD_ROWBLOCK && CH_ <= 16 && (CH_ + 3) / 4 * 2048 >= p.C)             \
+        hipLaunchKernelGGL((ln_bwd_rb_kernel<E, (CH_ + 3) / 4>), dim3(bwd_grid), dim3(256), 0, st, p); \
+      else                                                                             \
+        hipLaunchKernelGGL((ln_bwd_kernel<E, CH_>), dim3(bwd_grid), dim3(256), 0, st, p); \
       if (p.partial) {                                                                 \
         float* part2 = p.partial + (int64_t)bwd_grid * 2 * p.C;                        \
         const unsigned g = (unsigned)((2 * p.C + 255) / 256);                          \
@@ -430,6 +560,70 @@ __global__ __launch_bounds__(256) void dcoef_reduce_kernel(const float* part, fl
 
 int launch_dcoef_reduce(const float* part, float* dcoef, int H, int N, int64_t per, hipStream_t st) {
   hipLaunchKernelGGL(dcoef_reduce_kernel, dim3(H * N), dim3(256), 0, st, part, dcoef, per);
+  return (int)hipGetLastError();
+}
+
+// ---- SwiGLU (diff_transformer.py / Ndiff_transformer.py / control.py SwiGLU.forward):
+// out = silu(a) * b with a = linear_gate(x), b = linear_xform(x), and its backward
+// da = dout * b * silu'(a), db = dout * silu(a), silu'(a) = s (1 + a (1 - s)), s = sigmoid(a).
+// One pass each (PyTorch runs silu, mul, mul-backward and silu-backward as separate
+// passes); rows of a/b/out/dout/da/db may be strided views (row length n).  fp32 math.
+template <class E>
+__device__ __forceinline__ float silu_f(float a, float& sg) {
+  sg = 1.f / (1.f + __expf(-a));
+  return a * sg;
+}
+template <class E>
+__global__ __launch_bounds__(256) void swiglu_fwd_kernel(SwigluParams p) {
+  const int64_t per_row = p.n / 8, total = p.rows * per_row;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = i / per_row, c = (i % per_row) * 8;
+    float a[8], b[8], o[8];
+    ld8<E>(reinterpret_cast<const E*>(p.a) + r * p.as + c, a);
+    ld8<E>(reinterpret_cast<const E*>(p.b) + r * p.bs + c, b);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float sg;
+      o[j] = silu_f<E>(a[j], sg) * b[j];
+    }
+    st8<E>(reinterpret_cast<E*>(p.out) + r * p.os + c, o);
+  }
+}
+template <class E>
+__global__ __launch_bounds__(256) void swiglu_bwd_kernel(SwigluParams p) {
+  const int64_t per_row = p.n / 8, total = p.rows * per_row;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = i / per_row, c = (i % per_row) * 8;
+    float a[8], b[8], d[8], da[8], db[8];
+    ld8<E>(reinterpret_cast<const E*>(p.a) + r * p.as + c, a);
+    ld8<E>(reinterpret_cast<const E*>(p.b) + r * p.bs + c, b);
+    ld8<E>(reinterpret_cast<const E*>(p.dout) + r * p.dos + c, d);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float sg;
+      const float sl = silu_f<E>(a[j], sg);
+      db[j] = d[j] * sl;
+      da[j] = d[j] * b[j] * (sg * (1.f + a[j] * (1.f - sg)));
+    }
+    st8<E>(reinterpret_cast<E*>(p.da) + r * p.das + c, da);
+    st8<E>(reinterpret_cast<E*>(p.db) + r * p.dbs + c, db);
+  }
+}
+
+int launch_swiglu(int dtype, const SwigluParams& p, bool bwd, hipStream_t st) {
+  const int64_t items = p.rows * (p.n / 8);
+  if (items == 0) return 0;
+  dim3 g(grid_for(items));
+#define DTA_SW(E_)                                                                       \
+  if (bwd) hipLaunchKernelGGL(swiglu_bwd_kernel<E_>, g, dim3(256), 0, st, p);            \
+  else hipLaunchKernelGGL(swiglu_fwd_kernel<E_>, g, dim3(256), 0, st, p);
+  switch (dtype) {
+    case 0: DTA_SW(__bf16) break;
+    case 1: DTA_SW(_Float16) break;
+    case 2: DTA_SW(float) break;
+    default: return -2;
+  }
+#undef DTA_SW
   return (int)hipGetLastError();
 }
 

@@ -16,7 +16,7 @@ import torch.nn as nn
 from torch.nn import functional as F
 
 from . import kv_cache, ops
-from .packing import ensure_packed, packed_linear
+from .packing import ensure_packed, packed_linear, packed_tensor
 from ._compat import (emit_tril_hooks, lambda_init_value, check_seq_len, attn_dropout_p, fill_if_changed,
                       mha_out_scale)
 
@@ -106,6 +106,7 @@ class MultiHeadDiffAttention(nn.Module):
         self.head_size = head_size
         self.block_size = block_size
         self._pack = {}                            # the shared storage of the heads' projections
+        self._lam_pack = {}                        # ... and of their lambda vectors
 
     def packed_params(self):
         """Every head's projection weights in the kernel's packed row order."""
@@ -123,8 +124,17 @@ class MultiHeadDiffAttention(nn.Module):
         init = lambda_init_value(layer_idx, self.heads[0].lambda_init)
         for h in self.heads:                       # get_lambda's buffer side effect, every head
             fill_if_changed(h.lambda_init, init)
-        st = lambda name: torch.stack([getattr(h, name) for h in self.heads]).float()
-        return _layer_lambda_coef(st("lambda_q1"), st("lambda_k1"), st("lambda_q2"), st("lambda_k2"), init)
+        # the 4H lambda vectors are row views of one pack: one copy forward, one add backward
+        lam = packed_tensor(self.lambda_params(), self._lam_pack).view(4, self.num_heads, self.head_size).float()
+        return _layer_lambda_coef(lam[0], lam[1], lam[2], lam[3], init)
+
+    def lambda_params(self):
+        return ([h.lambda_q1 for h in self.heads] + [h.lambda_k1 for h in self.heads]
+                + [h.lambda_q2 for h in self.heads] + [h.lambda_k2 for h in self.heads])
+
+    def param_packs(self):
+        """(holder, params) of every shared-storage parameter group (dp.BucketedAllReduce)."""
+        return [(self._pack, self.packed_params()), (self._lam_pack, self.lambda_params())]
 
     def forward(self, x, layer_idx):
         check_seq_len(x.shape[1], self.block_size)
@@ -147,7 +157,7 @@ class SwiGLU(nn.Module):
         self.linear_xform = nn.Linear(size_in, size_out)
 
     def forward(self, x):
-        return F.silu(self.linear_gate(x)) * self.linear_xform(x)
+        return ops.swiglu(self.linear_gate(x), self.linear_xform(x))
 
 
 class Block(nn.Module):
@@ -158,8 +168,8 @@ class Block(nn.Module):
         head_size = n_embd // (n_head * 2)
         self.diff_attn = MultiHeadDiffAttention(n_head, head_size, n_embd, dropout, block_size)
         self.ffwd = nn.Sequential(SwiGLU(n_embd, 4 * n_embd), nn.Linear(4 * n_embd, n_embd), nn.Dropout(dropout))
-        self.ln1 = nn.LayerNorm(n_embd)
-        self.ln2 = nn.LayerNorm(n_embd)
+        self.ln1 = ops.LayerNorm(n_embd)
+        self.ln2 = ops.LayerNorm(n_embd)
 
     def forward(self, x, layer_idx):
         x = x + self.diff_attn(self.ln1(x), layer_idx)
@@ -176,7 +186,7 @@ class DiffTransformer(nn.Module):
         self.token_embedding_table = nn.Embedding(vocab_size, n_embd)
         self.position_embedding_table = nn.Embedding(block_size, n_embd)
         self.blocks = nn.ModuleList([Block(n_embd, n_head, block_size, dropout) for _ in range(n_layer)])
-        self.ln_f = nn.LayerNorm(n_embd)
+        self.ln_f = ops.LayerNorm(n_embd)
         self.lm_head = nn.Linear(n_embd, vocab_size)
         self.apply(self._init_weights)
 

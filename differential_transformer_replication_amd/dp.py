@@ -19,6 +19,10 @@ Design
   accumulation micro-steps.
 * Buffers (``lambda_init``, ``freqs_cis``) are never broadcast per step; the
   reference's T x T ``tril`` does not exist here (SURVEY semantic 8).
+* Packed attention projections (``packing.py``): the per-head weights of one
+  module are laid out consecutively in pack order inside one bucket and bound
+  to it (``packing.bind_grad``), so their backward accumulates the module's whole
+  dW with one add and reports the parameters to ``_on_grad`` itself.
 """
 from __future__ import annotations
 
@@ -27,6 +31,8 @@ from typing import Dict, List, Optional
 
 import torch
 import torch.distributed as dist
+
+from . import packing
 
 
 class _Bucket:
@@ -48,14 +54,39 @@ class BucketedAllReduce:
         self.params = [p for p in module.parameters() if p.requires_grad]
         self._enabled = True
         cap = int(bucket_cap_mb * 1024 * 1024)
+        # units of bucket layout: single parameters, or a packed module's per-head
+        # weights in pack order (kept together, never split across buckets)
+        packs, pack_of = [], {}
+        for m in module.modules():
+            if hasattr(m, "param_packs"):
+                groups_m = m.param_packs()
+            elif hasattr(m, "packed_params") and isinstance(getattr(m, "_pack", None), dict):
+                groups_m = [(m._pack, m.packed_params())]
+            else:
+                continue
+            for holder, allp in groups_m:
+                pp = [p for p in allp if p.requires_grad]
+                if (pp and len(pp) == len(allp) and all(p.dtype == torch.float32 for p in pp)
+                        and not any(id(p) in pack_of for p in pp)):
+                    packs.append((holder, pp))
+                    for p in pp:
+                        pack_of[id(p)] = len(packs) - 1
+        units, seen = [], set()
+        for p in reversed(self.params):
+            k = pack_of.get(id(p))
+            if k is None:
+                units.append([p])
+            elif k not in seen:
+                seen.add(k)
+                units.append(packs[k][1])
         groups: List[List[torch.nn.Parameter]] = []
         cur, cur_bytes = [], 0
-        for p in reversed(self.params):
-            nb = p.numel() * 4
+        for u in units:
+            nb = sum(p.numel() for p in u) * 4
             if cur and cur_bytes + nb > cap:
                 groups.append(cur)
                 cur, cur_bytes = [], 0
-            cur.append(p)
+            cur.extend(u)
             cur_bytes += nb
         if cur:
             groups.append(cur)
@@ -76,6 +107,11 @@ class BucketedAllReduce:
                 self._owner[id(p)] = b
         for p in self.params:
             p.register_post_accumulate_grad_hook(self._on_grad)
+        for holder, pp in packs:
+            b = self._owner[id(pp[0])]
+            start = pp[0].grad.data_ptr() - b.flat.data_ptr()
+            n = sum(p.numel() for p in pp)
+            packing.bind_grad(holder, pp, b.flat[start // 4:start // 4 + n], self._on_grad)
         if broadcast_init and self.world > 1:
             # identical initial parameters on every rank (parameters only, once)
             with torch.no_grad():

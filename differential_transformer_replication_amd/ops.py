@@ -20,6 +20,7 @@ import math
 from typing import Dict, List, Optional, Tuple
 
 import torch
+from torch.nn import functional as F
 
 from . import _lib
 
@@ -235,6 +236,65 @@ class _GroupLNScale(torch.autograd.Function):
 
 def group_ln_scale(x: Tensor, w: Tensor, b: Tensor, eps: float = 1e-5, out_scale: float = 1.0) -> Tensor:
     return _GroupLNScale.apply(x, w, b, eps, out_scale)
+
+
+class LayerNorm(torch.nn.LayerNorm):
+    """``nn.LayerNorm`` of the Blocks (``ln1``/``ln2``/``ln_f``: diff_transformer.py:111-126,
+    Ndiff_transformer.py:164-179, control.py:92-111) on the HIP LN kernels for GPU
+    tensors: same parameters, ``state_dict`` keys and fp32 statistics; under autocast
+    it normalises in fp32 like ``F.layer_norm``'s autocast rule.  Host tensors (the
+    control model on the CPU) and shapes the kernels do not take keep PyTorch's."""
+
+    def forward(self, x: Tensor) -> Tensor:
+        C = x.shape[-1]
+        if (not x.is_cuda or len(self.normalized_shape) != 1 or self.weight is None or self.bias is None
+                or C % 8 or C > 8192):
+            return super().forward(x)
+        if torch.is_autocast_enabled("cuda") and x.dtype != torch.float32:
+            x = x.float()
+        with torch.autocast("cuda", enabled=False):
+            return _GroupLNScale.apply(x, self.weight, self.bias, self.eps, 1.0)
+
+
+class _SwiGLU(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a: Tensor, b: Tensor):
+        lib = _lib.load()
+        _require_gpu(a, b)
+        if a.shape != b.shape:
+            raise RuntimeError("SwiGLU branches must have one shape")
+        dt = torch.promote_types(a.dtype, b.dtype)
+        a2 = a.to(dt).contiguous().view(-1, a.shape[-1])
+        b2 = b.to(dt).contiguous().view(-1, a.shape[-1])
+        out = torch.empty_like(a2)
+        n = a2.shape[1]
+        sa = _lib.SwigluArgs(_lib.dtype_code(dt), a2.shape[0], n, a2.data_ptr(), n, b2.data_ptr(), n,
+                             out.data_ptr(), n, None, 0, None, 0, None, 0)
+        _lib.check(lib.dta_swiglu_fwd(sa, _lib.stream_handle(a.device)))
+        ctx.save_for_backward(a2, b2)
+        ctx.meta = (a.shape, a.dtype, b.dtype)
+        return out.view(a.shape)
+
+    @staticmethod
+    def backward(ctx, dout: Tensor):
+        lib = _lib.load()
+        a2, b2 = ctx.saved_tensors
+        shape, adt, bdt = ctx.meta
+        n = a2.shape[1]
+        d2 = dout.to(a2.dtype).contiguous().view(-1, n)
+        da, db = torch.empty_like(a2), torch.empty_like(b2)
+        sa = _lib.SwigluArgs(_lib.dtype_code(a2.dtype), a2.shape[0], n, a2.data_ptr(), n, b2.data_ptr(), n,
+                             None, 0, d2.data_ptr(), n, da.data_ptr(), n, db.data_ptr(), n)
+        _lib.check(lib.dta_swiglu_bwd(sa, _lib.stream_handle(a2.device)))
+        return da.view(shape).to(adt), db.view(shape).to(bdt)
+
+
+def swiglu(a: Tensor, b: Tensor) -> Tensor:
+    """``F.silu(a) * b`` in one pass forward and one backward (SwiGLU.forward of the
+    reference models); GPU tensors whose last dim is a multiple of 8."""
+    if not a.is_cuda or a.shape[-1] % 8 or a.shape != b.shape:
+        return F.silu(a) * b
+    return _SwiGLU.apply(a, b)
 
 
 # ------------------------------------------------------------------ decode ---

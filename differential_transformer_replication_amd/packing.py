@@ -16,6 +16,13 @@ by copy after initialisation).  Only their storage is shared:
 * ``packed_linear`` is an autograd Function over the pack whose backward
   returns each parameter's gradient as a row slice of one dW -- the same bf16
   GEMMs and casts autocast applies to an ``nn.Linear``.
+
+Packed gradient accumulation: when the parameters' ``.grad`` tensors are
+themselves consecutive rows of one buffer in pack order (``dp.BucketedAllReduce``
+lays its buckets out that way, see ``bind_grad``), the backward adds the whole dW
+into that buffer in ONE kernel (casting bf16 -> fp32 on the fly) and reports each
+parameter to the bucket's ready hook itself, instead of autograd running one
+``AccumulateGrad`` add per parameter (2H..(2N+1)H small launches per module).
 """
 from __future__ import annotations
 
@@ -54,10 +61,31 @@ def ensure_packed(params: Sequence[torch.nn.Parameter], holder: Dict[str, torch.
     return base
 
 
+def bind_grad(holder: Dict, params: Sequence[torch.nn.Parameter], gflat: torch.Tensor, on_ready) -> None:
+    """Declare ``gflat`` (1-D fp32, the params' numels in pack order) as the buffer
+    the params' ``.grad`` views live in, and ``on_ready(p)`` as the hook to call once
+    a parameter's gradient has been accumulated."""
+    holder["grad"] = gflat
+    holder["on_ready"] = on_ready
+
+
+def _grad_target(holder: Dict, params: Sequence[torch.nn.Parameter]):
+    g = holder.get("grad")
+    if g is None:
+        return None
+    ptr, off = g.data_ptr(), 0
+    for p in params:                      # still the bound views (not set_to_none / replaced)?
+        pg = p.grad
+        if pg is None or pg.data_ptr() != ptr + off * 4 or pg.dtype != torch.float32:
+            return None
+        off += p.numel()
+    return g if off == g.numel() else None
+
+
 class _PackedLinear(torch.autograd.Function):
     @staticmethod
     @torch.amp.custom_fwd(device_type="cuda")
-    def forward(ctx, x, base, *params):
+    def forward(ctx, x, base, holder, *params):
         dt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else x.dtype
         xc = x.to(dt)
         wc = base.to(dt)
@@ -67,6 +95,9 @@ class _PackedLinear(torch.autograd.Function):
         ctx.x_dtype = x.dtype
         ctx.rows = [p.shape[0] for p in params]
         ctx.w_dtype = base.dtype
+        bound = holder is not None and "grad" in holder
+        ctx.holder = holder if bound else None
+        ctx.params = params if bound else None
         return y
 
     @staticmethod
@@ -77,12 +108,54 @@ class _PackedLinear(torch.autograd.Function):
         with torch.autocast("cuda", enabled=False):
             dx = (dy @ wc).to(ctx.x_dtype) if ctx.needs_input_grad[0] else None
             dw = dy.reshape(-1, dy.shape[-1]).t() @ xc.reshape(-1, xc.shape[-1])
+        if ctx.holder is not None and all(ctx.needs_input_grad[3:]):
+            g = _grad_target(ctx.holder, ctx.params)
+            if g is not None:
+                g.view_as(dw).add_(dw)            # one launch, bf16 -> fp32 in the add
+                hook = ctx.holder["on_ready"]
+                for p in ctx.params:
+                    hook(p)
+                return (dx, None, None) + (None,) * len(ctx.rows)
         dw = dw.to(ctx.w_dtype)
         grads: List[torch.Tensor] = list(torch.split(dw, ctx.rows, 0))
-        return (dx, None, *grads)
+        return (dx, None, None, *grads)
+
+
+class _PackedParams(torch.autograd.Function):
+    """The pack itself as a differentiable tensor of its parameters (used for the
+    per-head lambda vectors): forward copies the small pack once (one launch instead
+    of a ``torch.stack`` per vector kind); backward splits -- or, when bound, adds the
+    whole gradient into the bound buffer in one launch."""
+
+    @staticmethod
+    def forward(ctx, base, holder, *params):
+        bound = holder is not None and "grad" in holder
+        ctx.holder = holder if bound else None
+        ctx.params = params if bound else None
+        ctx.shapes = [p.shape for p in params]
+        return base.clone()
+
+    @staticmethod
+    def backward(ctx, d):
+        if ctx.holder is not None and all(ctx.needs_input_grad[2:]):
+            g = _grad_target(ctx.holder, ctx.params)
+            if g is not None:
+                g.view_as(d).add_(d)
+                hook = ctx.holder["on_ready"]
+                for p in ctx.params:
+                    hook(p)
+                return (None, None) + (None,) * len(ctx.shapes)
+        rows = [sh[0] for sh in ctx.shapes]
+        return (None, None) + tuple(t.reshape(sh) for t, sh in zip(torch.split(d, rows, 0), ctx.shapes))
+
+
+def packed_tensor(params: Sequence[torch.nn.Parameter], holder: Dict[str, torch.Tensor]) -> torch.Tensor:
+    """The (sum of rows, ...) pack of ``params`` as one autograd-tracked tensor."""
+    base = ensure_packed(params, holder)
+    return _PackedParams.apply(base, holder, *params)
 
 
 def packed_linear(x: torch.Tensor, params: Sequence[torch.nn.Parameter], holder: Dict[str, torch.Tensor]):
     """``x @ cat(params).T`` without the cat: one GEMM over the shared pack."""
     base = ensure_packed(params, holder)
-    return _PackedLinear.apply(x, base, *params)
+    return _PackedLinear.apply(x, base, holder, *params)

@@ -212,6 +212,24 @@ typedef struct dta_attn_decode_args {
 int dta_attn_decode(const dta_attn_decode_args* a, void* stream);
 size_t dta_attn_decode_workspace_bytes(int32_t B, int32_t H, int32_t n_terms, int32_t head_size, int32_t dv,
                                        int32_t t_cap);
+/* SwiGLU of the Block feed-forward (diff_transformer.py SwiGLU.forward,
+ * Ndiff_transformer.py:86-93 equivalent, control.py:80-90): out = silu(a) * b over
+ * rows x n elements (n % 8 == 0; every row stride a multiple of 8 elements, every
+ * pointer 16-byte aligned), and its backward da = dout * b * silu'(a),
+ * db = dout * silu(a).  Unused pointers of the other direction may be NULL. */
+typedef struct {
+  int32_t dtype;
+  int64_t rows, n;
+  const void* a; int64_t a_stride;
+  const void* b; int64_t b_stride;
+  void* out; int64_t out_stride;
+  const void* dout; int64_t dout_stride;
+  void* da; int64_t da_stride;
+  void* db; int64_t db_stride;
+} dta_swiglu_args;
+int dta_swiglu_fwd(const dta_swiglu_args* a, void* stream);
+int dta_swiglu_bwd(const dta_swiglu_args* a, void* stream);
+
 /* Cast/copy a [b][t][h][i][d] tensor from fp32 to dtype (dQ finalisation). */
 int dta_cast_f32(int32_t dtype, int32_t B, int32_t T, int32_t H, int32_t n_terms,
                  int32_t head_size, const float* src, dta_tensor dst, void* stream);

@@ -212,3 +212,13 @@ def test_control_model_cpu_matches_golden(golden):
     loss.backward()
     for k, p in m.named_parameters():
         assert rel_err(p.grad, g[f"grad::{k}"]) < 1e-5, k
+
+
+def test_swiglu_args_rejected_without_gpu():
+    lib = _lib.load()
+    a = _lib.SwigluArgs()
+    a.dtype, a.rows, a.n = 0, 4, 12                     # n not a multiple of 8
+    assert lib.dta_swiglu_fwd(a, None) == -2
+    a.n = 16
+    assert lib.dta_swiglu_fwd(a, None) == -1            # null pointers
+    assert lib.dta_swiglu_bwd(None, None) == -1

@@ -1,0 +1,96 @@
+"""GPU parity of the Block-level kernels around the attention path: the block-per-row
+LayerNorm backward on many rows, the Blocks' ``LayerNorm`` (ln1/ln2/ln_f) on the HIP
+LN kernels, and the fused SwiGLU -- each against a float64 PyTorch reference of the
+reference model's op (diff_transformer.py SwiGLU / nn.LayerNorm)."""
+import pytest
+import torch
+from torch.nn import functional as F
+
+from conftest import rel_err
+from oracle import diffattn_oracle as orc
+from test_gpu_parity import TOL, DEV, _ops
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("rows,C", [(4099, 1024), (2051, 2048), (9000, 384), (1, 8192)])
+def test_ln_backward_many_rows(dtype, rows, C):
+    """Many rows per workgroup (odd counts: both parities of the double-buffered row
+    slot), the per-block partials and their ordered reduction."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(rows + C)
+    x = torch.randn(rows, C, generator=g) * 2 + 0.5
+    w = 1 + 0.1 * torch.randn(C, generator=g)
+    b = 0.1 * torch.randn(C, generator=g)
+    dy = torch.randn(rows, C, generator=g)
+    xq = x.to(dtype).double().requires_grad_(True)
+    w64, b64 = w.double().requires_grad_(True), b.double().requires_grad_(True)
+    ref = orc.group_layer_norm(xq, w64, b64) * 0.2
+    ref.backward(dy.to(dtype).double())
+    xg = x.to(dtype).to(DEV).requires_grad_(True)
+    wg, bg = w.to(DEV).requires_grad_(True), b.to(DEV).requires_grad_(True)
+    out = ops.group_ln_scale(xg, wg, bg, 1e-5, 0.2)
+    out.backward(dy.to(dtype).to(DEV))
+    tol = TOL[dtype]
+    assert rel_err(out.float().cpu(), ref) < tol
+    assert rel_err(xg.grad.float().cpu(), xq.grad) < tol
+    assert rel_err(wg.grad.cpu(), w64.grad) < tol
+    assert rel_err(bg.grad.cpu(), b64.grad) < tol
+
+
+@pytest.mark.parametrize("autocast", [False, True])
+def test_block_layernorm_matches_torch(autocast):
+    ops = _ops()
+    torch.manual_seed(3)
+    C = 768
+    ln = ops.LayerNorm(C).to(DEV)
+    with torch.no_grad():
+        ln.weight.normal_(1.0, 0.1)
+        ln.bias.normal_(0.0, 0.1)
+    ref = torch.nn.LayerNorm(C).double()
+    ref.load_state_dict({k: v.double().cpu() for k, v in ln.state_dict().items()})
+    x = torch.randn(4, 300, C) * 3
+    dy = torch.randn(4, 300, C)
+    xg = x.to(DEV).requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=autocast):
+        y = ln(xg)
+    assert y.dtype == torch.float32                     # fp32 statistics and output, as F.layer_norm
+    y.backward(dy.to(DEV))
+    x64 = x.double().requires_grad_(True)
+    r = ref(x64)
+    r.backward(dy.double())
+    assert rel_err(y.cpu(), r) < 1e-5
+    assert rel_err(xg.grad.cpu(), x64.grad) < 1e-5
+    assert rel_err(ln.weight.grad.cpu(), ref.weight.grad) < 1e-5
+    assert rel_err(ln.bias.grad.cpu(), ref.bias.grad) < 1e-5
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+def test_swiglu_matches_torch(dtype):
+    ops = _ops()
+    g = torch.Generator().manual_seed(7)
+    a = torch.randn(3, 129, 1536, generator=g) * 3
+    b = torch.randn(3, 129, 1536, generator=g)
+    d = torch.randn(3, 129, 1536, generator=g)
+    a64 = a.to(dtype).double().requires_grad_(True)
+    b64 = b.to(dtype).double().requires_grad_(True)
+    r = F.silu(a64) * b64
+    r.backward(d.to(dtype).double())
+    ag = a.to(dtype).to(DEV).requires_grad_(True)
+    bg = b.to(dtype).to(DEV).requires_grad_(True)
+    out = ops.swiglu(ag, bg)
+    assert out.dtype == dtype
+    out.backward(d.to(dtype).to(DEV))
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert rel_err(out.float().cpu(), r) < tol
+    assert rel_err(ag.grad.float().cpu(), a64.grad) < tol
+    assert rel_err(bg.grad.float().cpu(), b64.grad) < tol
+
+
+def test_swiglu_module_uses_fused_kernel():
+    """The Block's SwiGLU module routes through dta_swiglu (autograd node _SwiGLU)."""
+    from differential_transformer_replication_amd import diff_transformer as D
+    m = D.SwiGLU(64, 256).to(DEV)
+    y = m(torch.randn(2, 5, 64, device=DEV))
+    assert type(y.grad_fn).__name__ == "_SwiGLUBackward"
