@@ -143,7 +143,7 @@ class MultiHeadAlternatingDiffAttention(nn.Module):
         # the 2NH lambda vectors are row views of one pack: one copy forward, one add backward
         lam = packed_tensor(self.lambda_params(), self._lam_pack).view(
             2, self.num_heads, self.n_terms, self.head_size).float()
-        return alternating_coefficients(lam[0], lam[1], init)
+        return alternating_coefficients(*lam.unbind(0), init)
 
     def lambda_params(self):
         return [p for h in self.heads for p in h.lambda_qs] + [p for h in self.heads for p in h.lambda_ks]
@@ -162,7 +162,7 @@ class MultiHeadAlternatingDiffAttention(nn.Module):
         out = ops.diff_attention(qkv, coef, self.num_heads, self.n_terms, self.head_size, freqs,
                                  dropout_p=attn_dropout_p([h.dropout for h in self.heads], self.training))
         gn = self.group_norm
-        out = ops.group_ln_scale(out, gn.weight, gn.bias, gn.eps, mha_out_scale(self.lambda_init))
+        out = ops.group_ln_scale(out, gn.weight, gn.bias, gn.eps, mha_out_scale(self.lambda_init), gn._gpack)
         return self.dropout(self.proj(out))
 
 
@@ -174,8 +174,8 @@ class Block(nn.Module):
         head_size = n_embd // (n_head * 2)
         self.diff_attn = MultiHeadAlternatingDiffAttention(n_head, head_size, n_embd, dropout, block_size, n_terms)
         self.ffwd = nn.Sequential(SwiGLU(n_embd, 4 * n_embd), nn.Linear(4 * n_embd, n_embd), nn.Dropout(dropout))
-        self.ln1 = ops.LayerNorm(n_embd)
-        self.ln2 = ops.LayerNorm(n_embd)
+        self.ln1 = ops.LayerNorm(n_embd, autocast_out=True)
+        self.ln2 = ops.LayerNorm(n_embd, autocast_out=True)
 
     def forward(self, x, layer_idx):
         x = x + self.diff_attn(self.ln1(x), layer_idx)
@@ -191,7 +191,7 @@ class AlternatingDiffTransformer(nn.Module):
         self.block_size = block_size
         self.token_embedding_table = nn.Embedding(vocab_size, n_embd)
         self.blocks = nn.ModuleList([Block(n_embd, n_head, block_size, dropout, n_terms) for _ in range(n_layer)])
-        self.ln_f = ops.LayerNorm(n_embd)
+        self.ln_f = ops.LayerNorm(n_embd, autocast_out=True)
         self.lm_head = nn.Linear(n_embd, vocab_size)
         self.apply(self._init_weights)
 

@@ -76,7 +76,7 @@ class LnArgs(ctypes.Structure):
                 ("mean", ctypes.c_void_p), ("rstd", ctypes.c_void_p),
                 ("dy", ctypes.c_void_p), ("dy_stride", ctypes.c_int64),
                 ("dx", ctypes.c_void_p), ("dx_stride", ctypes.c_int64),
-                ("dw", ctypes.c_void_p), ("db", ctypes.c_void_p), ("partial", ctypes.c_void_p)]
+                ("dw", ctypes.c_void_p), ("db", ctypes.c_void_p), ("partial", ctypes.c_void_p), ("io_dtype", ctypes.c_int32)]
 
 
 class RopeArgs(ctypes.Structure):

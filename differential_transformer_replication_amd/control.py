@@ -129,8 +129,8 @@ class Block(nn.Module):
         super().__init__()
         self.attn = MultiHeadAttention(n_head, n_embd // n_head, n_embd, dropout, block_size)
         self.ffwd = nn.Sequential(SwiGLU(n_embd, 4 * n_embd), nn.Linear(4 * n_embd, n_embd), nn.Dropout(dropout))
-        self.ln1 = ops.LayerNorm(n_embd)
-        self.ln2 = ops.LayerNorm(n_embd)
+        self.ln1 = ops.LayerNorm(n_embd, autocast_out=True)
+        self.ln2 = ops.LayerNorm(n_embd, autocast_out=True)
 
     def forward(self, x):
         x = x + self.attn(self.ln1(x))
@@ -145,7 +145,7 @@ class StandardTransformer(nn.Module):
         self.block_size = block_size
         self.token_embedding_table = nn.Embedding(vocab_size, n_embd)
         self.blocks = nn.ModuleList([Block(n_embd, n_head, block_size, dropout) for _ in range(n_layer)])
-        self.ln_f = ops.LayerNorm(n_embd)
+        self.ln_f = ops.LayerNorm(n_embd, autocast_out=True)
         self.lm_head = nn.Linear(n_embd, vocab_size)
         self.apply(self._init_weights)
 

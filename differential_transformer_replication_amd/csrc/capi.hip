@@ -252,6 +252,8 @@ int dta_attn_bwd(const dta_attn_bwd_args* a, void* stream) {
 
 static int ln_common(const dta_ln_args* a, bool bwd) {
   if (!a || a->dtype < DTA_BF16 || a->dtype > DTA_F32 || a->rows < 0 || a->C <= 0) return DTA_ERR_INVALID;
+  if (a->io_dtype != 0 && (a->dtype != DTA_F32 || (a->io_dtype - 1 != DTA_BF16 && a->io_dtype - 1 != DTA_F16)))
+    return DTA_ERR_UNSUPPORTED;
   const int64_t v = 8;   // kernels move 8 elements per lane access
   if (a->C % v || a->C > 8192) return DTA_ERR_UNSUPPORTED;
   if (!aligned_ptr(a->x) || a->x_stride % v || !a->w || !a->mean || !a->rstd) return DTA_ERR_INVALID;
@@ -274,6 +276,7 @@ static LnParams ln_params(const dta_ln_args* a) {
 
 int dta_ln_fwd(const dta_ln_args* a, void* stream) {
   if (int e = ln_common(a, false)) return e;
+  if (a->io_dtype) return status(launch_ln_mixed(a->io_dtype - 1, ln_params(a), false, (hipStream_t)stream));
   return status(launch_ln(a->dtype, ln_params(a), false, (hipStream_t)stream));
 }
 
@@ -281,6 +284,7 @@ size_t dta_ln_bwd_workspace_bytes(int64_t rows, int64_t C) { return (size_t)ln_b
 
 int dta_ln_bwd(const dta_ln_args* a, void* stream) {
   if (int e = ln_common(a, true)) return e;
+  if (a->io_dtype) return status(launch_ln_mixed(a->io_dtype - 1, ln_params(a), true, (hipStream_t)stream));
   return status(launch_ln(a->dtype, ln_params(a), true, (hipStream_t)stream));
 }
 

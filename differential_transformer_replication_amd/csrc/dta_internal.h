@@ -64,6 +64,7 @@ struct LnParams {
   float* dw; float* db;
   float* partial;      // optional [blocks][2][C] workspace: deterministic dw/db (no atomics)
 };
+int launch_ln_mixed(int y_dtype, const LnParams& p, bool bwd, hipStream_t st);   // x fp32, y / dy 16-bit
 int ln_bwd_blocks(int64_t rows);
 int64_t ln_bwd_workspace_floats(int64_t rows, int64_t C);
 

@@ -54,7 +54,7 @@ __device__ __forceinline__ float wave_sum(float v) {
 
 
 // CH = 8-element chunks per lane (C <= 512*CH)
-template <class E, int CH>
+template <class E, int CH, class Y = E>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(LnParams p) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -85,7 +85,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(LnParams p) {
   const float var = wave_sum(ss) * inv_c;
   const float rstd = 1.f / sqrtf(var + p.eps);
   if (lane == 0) { p.mean[row] = mean; p.rstd[row] = rstd; }
-  E* y = reinterpret_cast<E*>(p.y) + row * p.ys;
+  Y* y = reinterpret_cast<Y*>(p.y) + row * p.ys;
 #pragma unroll
   for (int c = 0; c < CH; ++c) {
     const int col = (c * 64 + lane) * 8;
@@ -94,7 +94,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(LnParams p) {
 #pragma unroll
       for (int j = 0; j < 8; ++j)
         o[j] = fmaf((v[c][j] - mean) * rstd, p.w[col + j], p.b[col + j]) * p.out_scale;
-      st8<E>(y + col, o);
+      st8<Y>(y + col, o);
     }
   }
 }
@@ -227,7 +227,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnParams p) {
 // buffered LDS slot, one barrier per row.  The next row's x / dy are loaded before
 // the current row's math.  ~60 VGPRs: 4 workgroups (16 waves) per CU, where the
 // wave-per-row kernel above holds 222 registers for C = 2048 (8 waves per CU).
-template <class E, int CHB>
+template <class E, int CHB, class Y = E>
 __global__ __launch_bounds__(256) void ln_bwd_rb_kernel(LnParams p) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   float dwp[CHB][8], dbp[CHB][8];
@@ -237,29 +237,32 @@ __global__ __launch_bounds__(256) void ln_bwd_rb_kernel(LnParams p) {
     for (int j = 0; j < 8; ++j) { dwp[c][j] = 0.f; dbp[c][j] = 0.f; }
   const float inv_c = 1.f / (float)p.C;
   __shared__ float red[2][4][2];
-  constexpr bool P16 = sizeof(E) == 2;
+  // raw (unconverted) vectors of 8 elements: one s16x8 for 16-bit, two f32x4 for fp32
+  constexpr bool P16 = sizeof(E) == 2, Y16 = sizeof(Y) == 2;
   typedef typename std::conditional<P16, s16x8, f32x4>::type RT;
-  constexpr int NR = P16 ? 1 : 2;                        // raw vectors per 8 elements
-  RT xr[2][CHB][NR], dr[2][CHB][NR];
+  typedef typename std::conditional<Y16, s16x8, f32x4>::type RY;
+  constexpr int NR = P16 ? 1 : 2, NY = Y16 ? 1 : 2;
+  RT xr[2][CHB][NR];
+  RY dr[2][CHB][NY];
   auto load = [&](auto S, int64_t r) {
     constexpr int s = decltype(S)::value;
     const E* x = reinterpret_cast<const E*>(p.x) + r * p.xs;
-    const E* dy = reinterpret_cast<const E*>(p.dy) + r * p.dys;
+    const Y* dy = reinterpret_cast<const Y*>(p.dy) + r * p.dys;
 #pragma unroll
     for (int c = 0; c < CHB; ++c) {
       const int col = (c * 256 + t) * 8;
       if (col < p.C) {
 #pragma unroll
-        for (int k = 0; k < NR; ++k) {
-          xr[s][c][k] = *reinterpret_cast<const RT*>(x + col + k * 4);
-          dr[s][c][k] = *reinterpret_cast<const RT*>(dy + col + k * 4);
-        }
+        for (int k = 0; k < NR; ++k) xr[s][c][k] = *reinterpret_cast<const RT*>(x + col + k * 4);
+#pragma unroll
+        for (int k = 0; k < NY; ++k) dr[s][c][k] = *reinterpret_cast<const RY*>(dy + col + k * 4);
       }
     }
   };
-  auto cvt = [&](const RT (&v)[NR], float* f) {
-    if constexpr (P16) {
-      raw_cvt<E>(v[0], f);
+  auto cvt = [&](auto T16, const auto& v, float* f) {
+    using V = decltype(T16);
+    if constexpr (sizeof(V) == 2) {
+      raw_cvt<V>(v[0], f);
     } else {
 #pragma unroll
       for (int j = 0; j < 4; ++j) { f[j] = v[0][j]; f[j + 4] = v[1][j]; }
@@ -278,8 +281,8 @@ __global__ __launch_bounds__(256) void ln_bwd_rb_kernel(LnParams p) {
       const int col = (c * 256 + t) * 8;
       if (col < p.C) {
         float xv[8], dv[8];
-        cvt(xr[s][c], xv);
-        cvt(dr[s][c], dv);
+        cvt(E{}, xr[s][c], xv);
+        cvt(Y{}, dr[s][c], dv);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           xh[c][j] = (xv[j] - mean) * rstd;
@@ -496,6 +499,41 @@ int ln_launch(const LnParams& p, bool bwd, hipStream_t st) {
   }
   DTA_LN(1) DTA_LN(2) DTA_LN(4) DTA_LN(8) DTA_LN(16)
 #undef DTA_LN
+  return -2;
+}
+
+// fp32 x / dx with 16-bit y / dy (block-per-row backward only)
+template <class Y>
+int ln_launch_mixed(const LnParams& p, bool bwd, hipStream_t st) {
+  const int64_t ch = (p.C + 511) / 512;
+  const int fwd_grid = (int)((p.rows + 3) / 4);
+  const int bwd_grid = ln_bwd_blocks(p.rows);
+#define DTA_LNM(CH_)                                                                             \
+  if (ch <= CH_) {                                                                               \
+    if (bwd) {                                                                                   \
+      hipLaunchKernelGGL((ln_bwd_rb_kernel<float, (CH_ + 3) / 4, Y>), dim3(bwd_grid), dim3(256), 0, st, p); \
+      if (p.partial) {                                                                           \
+        float* part2 = p.partial + (int64_t)bwd_grid * 2 * p.C;                                  \
+        const unsigned g = (unsigned)((2 * p.C + 255) / 256);                                    \
+        hipLaunchKernelGGL(ln_bwd_reduce1_kernel, dim3(g, kLnChunks), dim3(256), 0, st, p.partial, bwd_grid, p.C, part2); \
+        hipLaunchKernelGGL(ln_bwd_reduce2_kernel, dim3(g), dim3(256), 0, st, part2, p.C, p.dw, p.db); \
+      }                                                                                          \
+    } else {                                                                                     \
+      hipLaunchKernelGGL((ln_fwd_kernel<float, CH_, Y>), dim3(fwd_grid), dim3(256), 0, st, p);  \
+    }                                                                                            \
+    return (int)hipGetLastError();                                                               \
+  }
+  DTA_LNM(1) DTA_LNM(2) DTA_LNM(4) DTA_LNM(8) DTA_LNM(16)
+#undef DTA_LNM
+  return -2;
+}
+
+int launch_ln_mixed(int y_dtype, const LnParams& p, bool bwd, hipStream_t st) {
+  if (p.rows == 0) return 0;
+  switch (y_dtype) {
+    case 0: return ln_launch_mixed<__bf16>(p, bwd, st);
+    case 1: return ln_launch_mixed<_Float16>(p, bwd, st);
+  }
   return -2;
 }
 

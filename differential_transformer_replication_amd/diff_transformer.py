@@ -35,9 +35,13 @@ class GroupLayerNorm(nn.Module):
         width = num_heads * self.head_dim
         self.weight = nn.Parameter(torch.ones(1, 1, width))
         self.bias = nn.Parameter(torch.zeros(1, 1, width))
+        self._gpack = {}                           # grad binding of (weight, bias), dp.BucketedAllReduce
+
+    def param_packs(self):
+        return [(self._gpack, [self.weight, self.bias])]
 
     def forward(self, x):
-        return ops.group_ln_scale(x, self.weight, self.bias, self.eps, 1.0)
+        return ops.group_ln_scale(x, self.weight, self.bias, self.eps, 1.0, self._gpack)
 
 
 def _layer_lambda_coef(lq1, lk1, lq2, lk2, init: torch.Tensor) -> torch.Tensor:
@@ -126,7 +130,7 @@ class MultiHeadDiffAttention(nn.Module):
             fill_if_changed(h.lambda_init, init)
         # the 4H lambda vectors are row views of one pack: one copy forward, one add backward
         lam = packed_tensor(self.lambda_params(), self._lam_pack).view(4, self.num_heads, self.head_size).float()
-        return _layer_lambda_coef(lam[0], lam[1], lam[2], lam[3], init)
+        return _layer_lambda_coef(*lam.unbind(0), init)
 
     def lambda_params(self):
         return ([h.lambda_q1 for h in self.heads] + [h.lambda_k1 for h in self.heads]
@@ -144,7 +148,7 @@ class MultiHeadDiffAttention(nn.Module):
                                  dropout_p=attn_dropout_p([h.dropout for h in self.heads], self.training))
         # GroupLayerNorm then x(1 - lambda_init) with the MHA's own, never-updated 0.8 buffer
         gn = self.group_norm
-        out = ops.group_ln_scale(out, gn.weight, gn.bias, gn.eps, mha_out_scale(self.lambda_init))
+        out = ops.group_ln_scale(out, gn.weight, gn.bias, gn.eps, mha_out_scale(self.lambda_init), gn._gpack)
         return self.dropout(self.proj(out))
 
 
@@ -168,8 +172,8 @@ class Block(nn.Module):
         head_size = n_embd // (n_head * 2)
         self.diff_attn = MultiHeadDiffAttention(n_head, head_size, n_embd, dropout, block_size)
         self.ffwd = nn.Sequential(SwiGLU(n_embd, 4 * n_embd), nn.Linear(4 * n_embd, n_embd), nn.Dropout(dropout))
-        self.ln1 = ops.LayerNorm(n_embd)
-        self.ln2 = ops.LayerNorm(n_embd)
+        self.ln1 = ops.LayerNorm(n_embd, autocast_out=True)
+        self.ln2 = ops.LayerNorm(n_embd, autocast_out=True)
 
     def forward(self, x, layer_idx):
         x = x + self.diff_attn(self.ln1(x), layer_idx)
@@ -186,7 +190,7 @@ class DiffTransformer(nn.Module):
         self.token_embedding_table = nn.Embedding(vocab_size, n_embd)
         self.position_embedding_table = nn.Embedding(block_size, n_embd)
         self.blocks = nn.ModuleList([Block(n_embd, n_head, block_size, dropout) for _ in range(n_layer)])
-        self.ln_f = ops.LayerNorm(n_embd)
+        self.ln_f = ops.LayerNorm(n_embd, autocast_out=True)
         self.lm_head = nn.Linear(n_embd, vocab_size)
         self.apply(self._init_weights)
 

@@ -22,7 +22,7 @@ from typing import Dict, List, Optional, Tuple
 import torch
 from torch.nn import functional as F
 
-from . import _lib
+from . import _lib, packing
 
 Tensor = torch.Tensor
 
@@ -194,9 +194,13 @@ def diff_attention(qkv: Tensor, coef: Tensor, H: int, N: int, hs: int,
 
 class _GroupLNScale(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x: Tensor, w: Tensor, b: Tensor, eps: float, out_scale: float):
+    def forward(ctx, x: Tensor, w: Tensor, b: Tensor, eps: float, out_scale: float, holder=None,
+                y_dtype: Optional[torch.dtype] = None):
         lib = _lib.load()
         _require_gpu(x, w, b)
+        # bound (dp.BucketedAllReduce, packing.bind_grad): dw/db accumulate straight into
+        # the parameters' bucket-view gradients -- no zeros, no AccumulateGrad adds
+        ctx.bound = (holder, (w, b)) if holder is not None and "grad" in holder else None
         C = x.shape[-1]
         x2 = x.contiguous().view(-1, C)
         rows = x2.shape[0]
@@ -204,12 +208,20 @@ class _GroupLNScale(torch.autograd.Function):
         b32 = b.detach().to(torch.float32).contiguous().view(-1)
         if w32.numel() != C or b32.numel() != C:
             raise RuntimeError("GroupLayerNorm weight/bias size must equal the normalised width")
-        y = torch.empty_like(x2)
+        # io: an fp32 input normalised straight into a 16-bit output (and its backward
+        # from that dtype's gradient), dta_ln_args.io_dtype
+        io = 0
+        if y_dtype is not None and y_dtype != x.dtype:
+            if x.dtype != torch.float32 or y_dtype not in (torch.bfloat16, torch.float16):
+                raise RuntimeError("LayerNorm output dtype may differ only for fp32 input and 16-bit output")
+            io = 1 + _lib.dtype_code(y_dtype)
+        y = torch.empty(x2.shape, device=x.device, dtype=y_dtype if io else x.dtype)
         mean = torch.empty(rows, device=x.device, dtype=torch.float32)
         rstd = torch.empty_like(mean)
         a = _lib.LnArgs(_lib.dtype_code(x.dtype), rows, C, eps, out_scale, x2.data_ptr(), C, y.data_ptr(), C,
                         w32.data_ptr(), b32.data_ptr(), mean.data_ptr(), rstd.data_ptr(), None, 0, None, 0,
-                        None, None)
+                        None, None, None, io)
+        ctx.io = (io, y.dtype)
         _lib.check(lib.dta_ln_fwd(a, _lib.stream_handle(x.device)))
         ctx.save_for_backward(x2, w32, mean, rstd)
         ctx.meta = (eps, out_scale, x.shape, w.dtype, w.shape, b.dtype, b.shape)
@@ -221,21 +233,38 @@ class _GroupLNScale(torch.autograd.Function):
         x2, w32, mean, rstd = ctx.saved_tensors
         eps, out_scale, xshape, wdt, wshape, bdt, bshape = ctx.meta
         C = x2.shape[1]
-        dy2 = dy.to(x2.dtype).contiguous().view(-1, C)
+        io, ydt = ctx.io
+        dy2 = dy.to(ydt).contiguous().view(-1, C)
         dx = torch.empty_like(x2)
-        dw = torch.zeros(C, device=x2.device, dtype=torch.float32)
-        db = torch.zeros(C, device=x2.device, dtype=torch.float32)
+        g = None
+        if ctx.bound is not None and ctx.needs_input_grad[1] and ctx.needs_input_grad[2]:
+            holder, params = ctx.bound
+            g = packing._grad_target(holder, params)
+            if g is not None and g.numel() != 2 * C:
+                g = None
+        if g is not None:
+            dw, db = g[:C], g[C:]
+        else:
+            dw = torch.zeros(C, device=x2.device, dtype=torch.float32)
+            db = torch.zeros(C, device=x2.device, dtype=torch.float32)
         # per-block column partials summed in order: reproducible dw / db (no atomics)
         part = torch.empty(lib.dta_ln_bwd_workspace_bytes(x2.shape[0], C) // 4, device=x2.device, dtype=torch.float32)
         a = _lib.LnArgs(_lib.dtype_code(x2.dtype), x2.shape[0], C, eps, out_scale, x2.data_ptr(), C, None, 0,
                         w32.data_ptr(), None, mean.data_ptr(), rstd.data_ptr(), dy2.data_ptr(), C,
-                        dx.data_ptr(), C, dw.data_ptr(), db.data_ptr(), part.data_ptr())
+                        dx.data_ptr(), C, dw.data_ptr(), db.data_ptr(), part.data_ptr(), io)
         _lib.check(lib.dta_ln_bwd(a, _lib.stream_handle(x2.device)))
-        return dx.view(xshape), dw.to(wdt).view(wshape), db.to(bdt).view(bshape), None, None
+        if g is not None:
+            hook = ctx.bound[0]["on_ready"]
+            for p in ctx.bound[1]:
+                hook(p)
+            return dx.view(xshape), None, None, None, None, None, None
+        return dx.view(xshape), dw.to(wdt).view(wshape), db.to(bdt).view(bshape), None, None, None, None
 
 
-def group_ln_scale(x: Tensor, w: Tensor, b: Tensor, eps: float = 1e-5, out_scale: float = 1.0) -> Tensor:
-    return _GroupLNScale.apply(x, w, b, eps, out_scale)
+def group_ln_scale(x: Tensor, w: Tensor, b: Tensor, eps: float = 1e-5, out_scale: float = 1.0,
+                   holder: Optional[Dict] = None) -> Tensor:
+    """``holder``: the module's grad-binding dict (``param_packs``), or None."""
+    return _GroupLNScale.apply(x, w, b, eps, out_scale, holder, None)
 
 
 class LayerNorm(torch.nn.LayerNorm):
@@ -245,15 +274,30 @@ class LayerNorm(torch.nn.LayerNorm):
     it normalises in fp32 like ``F.layer_norm``'s autocast rule.  Host tensors (the
     control model on the CPU) and shapes the kernels do not take keep PyTorch's."""
 
+    def __init__(self, *args, autocast_out: bool = False, **kwargs):
+        super().__init__(*args, **kwargs)
+        self._gpack = {}                      # grad binding of (weight, bias), dp.BucketedAllReduce
+        # autocast_out: under autocast, write the output in the autocast dtype -- exact
+        # when every consumer is an autocast GEMM (which would cast it anyway: the
+        # Blocks' ln1/ln2/ln_f), and it saves the separate cast there and back
+        self.autocast_out = autocast_out
+
+    def param_packs(self):
+        return [(self._gpack, [self.weight, self.bias])] if self.weight is not None and self.bias is not None else []
+
     def forward(self, x: Tensor) -> Tensor:
         C = x.shape[-1]
         if (not x.is_cuda or len(self.normalized_shape) != 1 or self.weight is None or self.bias is None
                 or C % 8 or C > 8192):
             return super().forward(x)
-        if torch.is_autocast_enabled("cuda") and x.dtype != torch.float32:
-            x = x.float()
+        ydt = None
+        if torch.is_autocast_enabled("cuda"):
+            if x.dtype != torch.float32:
+                x = x.float()
+            if self.autocast_out:
+                ydt = torch.get_autocast_dtype("cuda")
         with torch.autocast("cuda", enabled=False):
-            return _GroupLNScale.apply(x, self.weight, self.bias, self.eps, 1.0)
+            return _GroupLNScale.apply(x, self.weight, self.bias, self.eps, 1.0, self._gpack, ydt)
 
 
 class _SwiGLU(torch.autograd.Function):

@@ -222,3 +222,15 @@ def test_swiglu_args_rejected_without_gpu():
     a.n = 16
     assert lib.dta_swiglu_fwd(a, None) == -1            # null pointers
     assert lib.dta_swiglu_bwd(None, None) == -1
+
+
+def test_ln_io_dtype_rules_without_gpu():
+    """A 16-bit y / dy beside an fp32 x only (dta_ln_args.io_dtype)."""
+    lib = _lib.load()
+    a = _lib.LnArgs()
+    a.dtype, a.rows, a.C, a.io_dtype = _lib.DTA_BF16, 4, 64, 1 + _lib.DTA_BF16
+    assert lib.dta_ln_fwd(a, None) == -2
+    a.dtype, a.io_dtype = _lib.DTA_F32, 1 + _lib.DTA_F32
+    assert lib.dta_ln_fwd(a, None) == -2
+    a.io_dtype = 1 + _lib.DTA_BF16
+    assert lib.dta_ln_fwd(a, None) == -1            # valid combination, null pointers

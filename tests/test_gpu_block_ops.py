@@ -66,6 +66,38 @@ def test_block_layernorm_matches_torch(autocast):
     assert rel_err(ln.bias.grad.cpu(), ref.bias.grad) < 1e-5
 
 
+@pytest.mark.parametrize("ydt", [torch.bfloat16, torch.float16])
+def test_block_layernorm_autocast_out(ydt):
+    """ln1/ln2/ln_f under autocast write the autocast dtype directly (fp32 statistics,
+    one rounding -- what the consuming GEMM's cast would produce) and take that
+    dtype's gradient back (dta_ln_args.io_dtype)."""
+    ops = _ops()
+    torch.manual_seed(4)
+    C = 1024
+    ln = ops.LayerNorm(C, autocast_out=True).to(DEV)
+    with torch.no_grad():
+        ln.weight.normal_(1.0, 0.1)
+        ln.bias.normal_(0.0, 0.1)
+    ref = torch.nn.LayerNorm(C).double()
+    ref.load_state_dict({k: v.double().cpu() for k, v in ln.state_dict().items()})
+    x = torch.randn(3, 257, C) * 2
+    dy = torch.randn(3, 257, C).to(ydt)
+    xg = x.to(DEV).requires_grad_(True)
+    with torch.autocast("cuda", dtype=ydt):
+        y = ln(xg)
+    assert y.dtype == ydt
+    y.backward(dy.to(DEV))
+    x64 = x.double().requires_grad_(True)
+    r = ref(x64)
+    r.backward(dy.double())
+    assert rel_err(y.float().cpu(), r) < 1e-2
+    # the output is the fp32 result rounded once
+    assert rel_err(y.float().cpu(), r.to(ydt).double()) < 1e-2
+    assert rel_err(xg.grad.cpu(), x64.grad) < 1e-5
+    assert rel_err(ln.weight.grad.cpu(), ref.weight.grad) < 1e-5
+    assert rel_err(ln.bias.grad.cpu(), ref.bias.grad) < 1e-5
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 def test_swiglu_matches_torch(dtype):
     ops = _ops()
@@ -94,3 +126,35 @@ def test_swiglu_module_uses_fused_kernel():
     m = D.SwiGLU(64, 256).to(DEV)
     y = m(torch.randn(2, 5, 64, device=DEV))
     assert type(y.grad_fn).__name__ == "_SwiGLUBackward"
+
+
+@pytest.mark.parametrize("arch", ["diff", "ndiff"])
+def test_bound_gradients_equal_autograd(arch):
+    """The DP buckets' one-add paths (packed projection weights, packed lambda
+    vectors, LayerNorm / GroupLayerNorm dw-db accumulated in place) give bitwise the
+    gradients plain autograd gives, over two accumulation micro-steps."""
+    from differential_transformer_replication_amd import diff_transformer as D, Ndiff_transformer as ND
+    from differential_transformer_replication_amd.dp import BucketedAllReduce
+
+    def build():
+        torch.manual_seed(0)
+        if arch == "diff":
+            return D.DiffTransformer(97, 64, 2, 2, 32, 0.0).to(DEV)
+        return ND.AlternatingDiffTransformer(97, 64, 2, 2, 32, 0.0, n_terms=3).to(DEV)
+
+    ref, m = build(), build()
+    for mod in (ref, m):
+        for p in mod.parameters():
+            if p.dim() == 1 and p.numel() == 16:
+                with torch.no_grad():
+                    p.copy_(torch.linspace(-0.2, 0.2, 16, device=DEV))
+    BucketedAllReduce(m, bucket_cap_mb=0.5)
+    g = torch.Generator().manual_seed(5)
+    for _ in range(2):
+        idx = torch.randint(0, 97, (2, 32), generator=g).to(DEV)
+        tgt = torch.randint(0, 97, (2, 32), generator=g).to(DEV)
+        ref(idx, tgt)[1].backward()
+        m(idx, tgt)[1].backward()
+    torch.cuda.synchronize()
+    for (n, a), (_, b) in zip(ref.named_parameters(), m.named_parameters()):
+        assert torch.equal(a.grad, b.grad), n
