@@ -45,6 +45,9 @@
 //   DTA_DKDV_STAGGER  waves 4-7 defer their dV product by one step   dK/dV 1.547 -> 1.747 ms (8 VGPR spill)
 //   DTA_FWD_LATE / DTA_DKDV_LATE   next tile's DMA after the compute  fwd 1.038 -> 1.035, dK/dV 1.564 -> 1.554 (noise)
 //   DTA_FWD_SPLIT / DTA_DKDV_SPLIT DMA slots spread over the step     fwd 1.010 -> 1.048, dK/dV 1.541 -> 1.616
+#ifndef DTA_DKDV_BQ          // 64: cfg2 dK/dV 1.543 -> 1.455 ms (one-process A/B)
+#define DTA_DKDV_BQ 64
+#endif
 #ifndef DTA_DKDV_STAGGER
 #define DTA_DKDV_STAGGER 0
 #endif
@@ -1638,9 +1641,14 @@ inline bool ring_layout_ok(const BwdParams& p, int es) {
 
 template <class E, int HS, int N, int DV, int NW>
 struct DkdvCfg {
-  static constexpr int BQ = 32;
   static constexpr int BK = NW * 32;
   static constexpr int HSP = HS < 32 ? 32 : HS;
+  // 64-row query stages (two 32-row sub-tiles per DMA round and barrier; 16-bit,
+  // DTA_DKDV_BQ = 64, the default) when K rows plus a 2-stage ring of them fit LDS;
+  // otherwise 32 (keeps the key block as wide as with 32-row stages)
+  static constexpr int BQ = (DTA_DKDV_BQ == 64 && sizeof(E) == 2 && HS >= 32 &&
+                             (N * BK * HS + 2 * (N * 64 * HSP + 64 * DV)) * (int)sizeof(E) +
+                                     2 * 2 * ((N * 64 + 63) / 64 * 64) * 4 <= 160 * 1024) ? 64 : 32;
   static constexpr int NP = (N * BQ + 63) / 64 * 64;      // fp32 row vectors, padded to DMA pieces
   static constexpr int nQ = N * BQ * HSP;
   static constexpr int nD = BQ * DV;
@@ -1694,7 +1702,8 @@ __global__ __launch_bounds__(NW * 64, (NW >= 8 ? 2 : 1)) void attn_dkdv_kernel(B
   float* Lb = reinterpret_cast<float*>(Db + NS * CF::nD);  // [NS][NP] lse
   float* Gb = Lb + NS * NP;                                 // [NS][NP] delta
   // SRD: the ring is instead NS stages of TileRing's layout, filled by buffer_load ... lds
-  using RG = TileRing<E, HS, N, DV, NW, DK>;
+  using RG = TileRing<E, HS, N, DV, NW, DK, BQ>;
+  constexpr int SUB = BQ / 32;            // 32-row sub-tiles per stage
   char* ringb = reinterpret_cast<char*>(Qb);
   static_assert(!SRD || (RG::ok && RG::SB * NS <= CF::bytes - CF::nK * (int)sizeof(E)), "ring layout");
 
@@ -1774,7 +1783,7 @@ __global__ __launch_bounds__(NW * 64, (NW >= 8 ? 2 : 1)) void attn_dkdv_kernel(B
   // Their dO tile t is still read in step t+1, so the ring prefetches one tile less
   // far ahead (LA = NS - 2): the slot refilled in step t held tile t-2, released by
   // every wave at the barrier closing step t-1.
-  constexpr bool STG = DTA_DKDV_STAGGER && NW == 8 && DVV && sizeof(E) == 2 && NS >= 3;
+  constexpr bool STG = DTA_DKDV_STAGGER && NW == 8 && DVV && sizeof(E) == 2 && NS >= 3 && SUB == 1;
   constexpr int LA = STG ? NS - 2 : NS - 1;
   const bool g1 = STG && wave >= NW / 2;
   for (int j = 0; j < LA; ++j)
@@ -1834,7 +1843,7 @@ __global__ __launch_bounds__(NW * 64, (NW >= 8 ? 2 : 1)) void attn_dkdv_kernel(B
     // DTA_DKDV_SPLIT: this wave's DMA pieces for tile t+NS-1 go out in three parts
     // spread over the step (after the barrier, after branch 0's S chain, before dV)
     // instead of all at once, so 8 waves do not queue their pieces together
-    constexpr bool SPLIT = DTA_DKDV_SPLIT && SRD && !DTA_DKDV_PREOFF && RG::MYP >= 2 && !STG;
+    constexpr bool SPLIT = DTA_DKDV_SPLIT && SRD && !DTA_DKDV_PREOFF && RG::MYP >= 2 && !STG && SUB == 1;
     const bool iss = t + LA < ntiles;
     auto issue_part = [&](auto UA, auto UB) {
       if (iss)
@@ -1851,12 +1860,23 @@ __global__ __launch_bounds__(NW * 64, (NW >= 8 ? 2 : 1)) void attn_dkdv_kernel(B
     st.lap<0>();
     const bool busy = wave_keys && q0 + BQ - 1 >= kw0;
     if constexpr (SPLIT) if (!busy) issue_part(U1{}, UM{});
-    if (busy) {
+    // BQ = 64: a stage holds two 32-row sub-tiles, computed one after the other with
+    // the same registers, so one DMA round, one wait and one barrier serve 64 rows
+    sfor<SUB>([&](auto USUB) {
+    constexpr int so = 32 * decltype(USUB)::value;
+    const int qs = q0 + so;                 // this sub-tile's first query row
+    if constexpr (SUB > 1) {
+      __builtin_amdgcn_sched_barrier(0);    // sub-tiles never interleave (registers)
+      asm volatile("" : "+v"(lane));        // and re-derive the lane addresses per sub-tile
+      hf = lane >> 5; c32 = lane & 31;
+      krow = kw0 + c32;
+    }
+    if (wave_keys && qs + 31 >= kw0) {
       const char* sg = ringb + buf * RG::SB;
-      const E* Qc = SRD ? reinterpret_cast<const E*>(sg) : Qb + buf * N * BQ * HSP;
-      const E* Dc = SRD ? reinterpret_cast<const E*>(sg + RG::OFF_D) : Db + buf * BQ * DV;
-      const float* Lc = SRD ? reinterpret_cast<const float*>(sg + RG::OFF_L) : Lb + buf * NP;
-      const float* Gc = SRD ? reinterpret_cast<const float*>(sg + RG::OFF_G) : Gb + buf * NP;
+      const E* Qc = (SRD ? reinterpret_cast<const E*>(sg) : Qb + buf * N * BQ * HSP) + so * HSP;
+      const E* Dc = (SRD ? reinterpret_cast<const E*>(sg + RG::OFF_D) : Db + buf * BQ * DV) + so * DV;
+      const float* Lc = (SRD ? reinterpret_cast<const float*>(sg + RG::OFF_L) : Lb + buf * NP) + so;
+      const float* Gc = (SRD ? reinterpret_cast<const float*>(sg + RG::OFF_G) : Gb + buf * NP) + so;
       {
       f32x16 dpa = f32x16{};
       if constexpr (DK) {
@@ -1873,8 +1893,8 @@ __global__ __launch_bounds__(NW * 64, (NW >= 8 ? 2 : 1)) void attn_dkdv_kernel(B
       st.lap<1>();
       f32x16 pc = f32x16{};
       // rows q0 + rowof(r) > lim are masked: query < key, or past the end
-      const int lim_lo = krow - q0 - 4 * hf;          // masked if rowof_c < lim_lo (query < key)
-      const int lim_hi = T - 1 - q0 - 4 * hf;         // masked if rowof_c > lim_hi (query >= T)
+      const int lim_lo = krow - qs - 4 * hf;          // masked if rowof_c < lim_lo (query < key)
+      const int lim_hi = T - 1 - qs - 4 * hf;         // masked if rowof_c > lim_hi (query >= T)
 #pragma unroll
       for (int i = 0; i < N; ++i) {
         f32x16 sa = f32x16{};
@@ -1917,7 +1937,7 @@ __global__ __launch_bounds__(NW * 64, (NW >= 8 ? 2 : 1)) void attn_dkdv_kernel(B
             }
             const float pr = exp2_fast(arg);
             float cm = coef[i];                 // dropout: this map element's kept weight c_i * mask/(1-p)
-            if constexpr (DROP) cm *= drop_mul(dkey[i], q0 + (r & 3) + 8 * (r >> 2) + 4 * hf, krow, p.drop_thr, p.drop_scale);
+            if constexpr (DROP) cm *= drop_mul(dkey[i], qs + (r & 3) + 8 * (r >> 2) + 4 * hf, krow, p.drop_thr, p.drop_scale);
             if constexpr (DVV) pc[r] = fmaf(cm, pr, pc[r]);
             if constexpr (DK) sa[r] = pr * fmaf(cm, dpa[r], -d4[j]);
           }
@@ -1985,6 +2005,7 @@ __global__ __launch_bounds__(NW * 64, (NW >= 8 ? 2 : 1)) void attn_dkdv_kernel(B
       }
       }
     }
+    });
     // DTA_DKDV_LATE: the next tile's DMA goes out after the compute, beside the barrier wait
     if constexpr (DTA_DKDV_LATE && !SPLIT) if (iss) stage_q(q0 + LA * BQ, (t + LA) % NS);
     st.lap<3>();
