@@ -464,6 +464,24 @@ inline bool kv_layout_ok(const P& p, int es) {
 }
 
 // ---------------------------------------------------------------- forward ---
+// Paired workgroups (DTA_*_PAIR): 4-wave workgroups sized to 80 KB of LDS, two per
+// CU, so the two waves sharing a SIMD belong to different workgroups (different
+// barriers) instead of one 8-wave workgroup whose SIMD partners run in lockstep
+// (MI355X_MICROARCH.md, two waves per SIMD).  The forward and dQ plans then take
+// 32-key tiles (Q stays in LDS: 32 KB + 3 x 16 KB).
+#ifndef DTA_DKDV_PAIR          // 1: cfg2 dK/dV 1.499 -> 1.406 ms (one-process A/B); fwd / dQ: slower, off
+#define DTA_DKDV_PAIR 1
+#endif
+#ifndef DTA_FWD_PAIR
+#define DTA_FWD_PAIR 0
+#endif
+#ifndef DTA_DQ_PAIR
+#define DTA_DQ_PAIR 0
+#endif
+constexpr int ring_stages_lim(int fixed_bytes, int tile_bytes, int lim) {
+  return (fixed_bytes + 4 * tile_bytes <= lim) ? 4 : (fixed_bytes + 3 * tile_bytes <= lim) ? 3 : 2;
+}
+
 template <class E> struct FwdTile { static constexpr int BN = 64; };
 template <> struct FwdTile<float> { static constexpr int BN = 32; };
 
@@ -476,12 +494,14 @@ struct FwdChunk {
 
 template <class E, int HS, int N, int DVC, int NW, bool QREG>
 struct FwdCfg {
-  static constexpr int BN = FwdTile<E>::BN;
+  static constexpr bool PAIR = DTA_FWD_PAIR && NW == 4 && !QREG && sizeof(E) == 2;
+  static constexpr int BN = PAIR ? 32 : FwdTile<E>::BN;
   static constexpr int BM = NW * 32;
   static constexpr int nQ = QREG ? 0 : N * BM * HS;
   static constexpr int nK = N * BN * HS;
   static constexpr int nV = BN * DVC;
-  static constexpr int NS = ring_stages(nQ * (int)sizeof(E), (nK + nV) * (int)sizeof(E));
+  static constexpr int NS = ring_stages_lim(nQ * (int)sizeof(E), (nK + nV) * (int)sizeof(E),
+                                            PAIR ? 80 * 1024 : 160 * 1024);
   static constexpr int bytes = (nQ + NS * nK + NS * nV) * (int)sizeof(E);
   // rough VGPR count (accumulators, two key blocks of scores, P, Q fragments,
   // addresses); a plan that fits 256 keeps the two-waves-per-SIMD bound
@@ -499,7 +519,9 @@ struct FwdPick {
   static constexpr bool q8 = NWMAX >= 8 && FwdCfg<E, HS, N, DVC, 8, false>::bytes <= LIM &&
                              FwdCfg<E, HS, N, DVC, 8, false>::regs <= 280;
   static constexpr bool q4 = FwdCfg<E, HS, N, DVC, 4, false>::bytes <= LIM;
-  static constexpr int NW = q8 ? 8 : (q4 ? 4 : 4);
+  static constexpr bool pair = DTA_FWD_PAIR && q8 && FwdCfg<E, HS, N, DVC, 4, false>::PAIR &&
+                                FwdCfg<E, HS, N, DVC, 4, false>::bytes <= 80 * 1024;
+  static constexpr int NW = pair ? 4 : (q8 ? 8 : (q4 ? 4 : 4));
   static constexpr bool QREG = !(q8 || q4);
   static constexpr bool ok = FwdCfg<E, HS, N, DVC, NW, QREG>::bytes <= LIM;
 };
@@ -1223,13 +1245,15 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_pipe_kernel(FwdParams p) {
 // ------------------------------------------------------ backward: dQ ---
 template <class E, int HS, int N, int DV, int NW, bool QREG>
 struct DqCfg {
-  static constexpr int BN = FwdTile<E>::BN;
+  static constexpr bool PAIR = DTA_DQ_PAIR && NW == 4 && !QREG && sizeof(E) == 2;
+  static constexpr int BN = PAIR ? 32 : FwdTile<E>::BN;
   static constexpr int BM = NW * 32;
   static constexpr int HSP = HS < 32 ? 32 : HS;
   static constexpr int nQ = QREG ? 0 : N * BM * HS;
   static constexpr int nK = N * BN * HSP;
   static constexpr int nV = BN * DV;
-  static constexpr int NS = ring_stages(nQ * (int)sizeof(E), (nK + nV) * (int)sizeof(E));
+  static constexpr int NS = ring_stages_lim(nQ * (int)sizeof(E), (nK + nV) * (int)sizeof(E),
+                                            PAIR ? 80 * 1024 : 160 * 1024);
   static constexpr int bytes = (nQ + NS * nK + NS * nV) * (int)sizeof(E);
 };
 
@@ -1237,8 +1261,9 @@ template <class E, int HS, int N, int DV = 2 * HS>
 struct DqPick {
   static constexpr int LIM = 160 * 1024;
   static constexpr bool q8 = sizeof(E) == 2 && DqCfg<E, HS, N, DV, 8, false>::bytes <= LIM;
-  static constexpr int NW = q8 ? 8 : (sizeof(E) == 2 ? 4 : 2);
-  static constexpr bool QREG = !q8;
+  static constexpr bool pair = DTA_DQ_PAIR && q8 && DqCfg<E, HS, N, DV, 4, false>::bytes <= 80 * 1024;
+  static constexpr int NW = pair ? 4 : (q8 ? 8 : (sizeof(E) == 2 ? 4 : 2));
+  static constexpr bool QREG = pair ? false : !q8;
   static constexpr bool ok = DqCfg<E, HS, N, DV, NW, QREG>::bytes <= LIM;
 };
 
@@ -1639,8 +1664,9 @@ inline bool ring_layout_ok(const BwdParams& p, int es) {
 
 // --------------------------------------------------- backward: dK, dV ---
 
-template <class E, int HS, int N, int DV, int NW>
+template <class E, int HS, int N, int DV, int NW, bool PR = false>
 struct DkdvCfg {
+  static constexpr int LIMB = PR ? 80 * 1024 : 160 * 1024;     // PR: paired 4-wave plan, two per CU
   static constexpr int BK = NW * 32;
   static constexpr int HSP = HS < 32 ? 32 : HS;
   // 64-row query stages (two 32-row sub-tiles per DMA round and barrier; 16-bit,
@@ -1648,13 +1674,13 @@ struct DkdvCfg {
   // otherwise 32 (keeps the key block as wide as with 32-row stages)
   static constexpr int BQ = (DTA_DKDV_BQ == 64 && sizeof(E) == 2 && HS >= 32 &&
                              (N * BK * HS + 2 * (N * 64 * HSP + 64 * DV)) * (int)sizeof(E) +
-                                     2 * 2 * ((N * 64 + 63) / 64 * 64) * 4 <= 160 * 1024) ? 64 : 32;
+                                     2 * 2 * ((N * 64 + 63) / 64 * 64) * 4 <= LIMB) ? 64 : 32;
   static constexpr int NP = (N * BQ + 63) / 64 * 64;      // fp32 row vectors, padded to DMA pieces
   static constexpr int nQ = N * BQ * HSP;
   static constexpr int nD = BQ * DV;
   static constexpr int nK = N * BK * HS;                   // the workgroup's K_i rows (B of S_i)
   // the stagger (DTA_DKDV_STAGGER) holds one stage longer: take a fifth when it fits
-  static constexpr int NS0 = ring_stages(nK * (int)sizeof(E), (nQ + nD) * (int)sizeof(E) + 2 * NP * 4);
+  static constexpr int NS0 = ring_stages_lim(nK * (int)sizeof(E), (nQ + nD) * (int)sizeof(E) + 2 * NP * 4, LIMB);
   static constexpr int NS = (DTA_DKDV_STAGGER && NS0 == 4 &&
                              nK * (int)sizeof(E) + 5 * ((nQ + nD) * (int)sizeof(E) + 2 * NP * 4) <= 160 * 1024) ? 5 : NS0;
   static constexpr int bytes = (nK + NS * nQ + NS * nD) * (int)sizeof(E) + NS * 2 * NP * 4;
@@ -1677,15 +1703,21 @@ struct DkdvWaves {
   static constexpr int HSP = HS < 32 ? 32 : HS;
   static constexpr int regs8 = DkdvSplit<HS, N, DV>::fused ? N * HSP / 2 + DV / 2 + DV / 4 + 88
                              : (N * HSP / 2 + DV / 4 > DV / 2 ? N * HSP / 2 + DV / 4 : DV / 2) + 88;
-  static constexpr int v = (sizeof(E) == 2 && DkdvCfg<E, HS, N, DV, 8>::bytes <= LIM && regs8 <= 256) ? 8
-                         : DkdvCfg<E, HS, N, DV, 4>::bytes <= LIM ? 4 : 2;
+  static constexpr int v8 = (sizeof(E) == 2 && DkdvCfg<E, HS, N, DV, 8>::bytes <= LIM && regs8 <= 256) ? 8
+                          : DkdvCfg<E, HS, N, DV, 4>::bytes <= LIM ? 4 : 2;
+  // DTA_DKDV_PAIR (default): where the 8-wave plan applies, two 4-wave workgroups per CU instead
+  // (bf16 only: the fp16 paired instantiation spills 16 VGPRs)
+  static constexpr bool pair = DTA_DKDV_PAIR && std::is_same<E, __bf16>::value && v8 == 8 &&
+                               DkdvCfg<E, HS, N, DV, 4, true>::bytes <= 80 * 1024;
+  static constexpr int v = pair ? 4 : v8;
 };
 
-template <class E, int HS, int N, int DV, int NW, bool DK, bool DVV, bool SRD, bool DROP>
-__global__ __launch_bounds__(NW * 64, (NW >= 8 ? 2 : 1)) void attn_dkdv_kernel(BwdParams p) {
+template <class E, int HS, int N, int DV, int NW, bool DK, bool DVV, bool SRD, bool DROP, bool PR>
+__global__ __launch_bounds__(NW * 64, (NW >= 8 || PR ? 2 : 1))
+void attn_dkdv_kernel(BwdParams p) {
   using O = Ops<E>;
   using frag = typename O::frag;
-  using CF = DkdvCfg<E, HS, N, DV, NW>;
+  using CF = DkdvCfg<E, HS, N, DV, NW, PR>;
   constexpr int HSP = CF::HSP, BQ = CF::BQ, BK = CF::BK, NP = CF::NP, NTHR = NW * 64;
   using QI = Img<E, HSP>;
   using DI = Img<E, DV>;
@@ -2352,7 +2384,8 @@ struct Plan {
   using FP = FwdPick<E, HS, N, DV>;
   using DP = DqPick<E, HS, N, DV>;
   static constexpr int KVW = DkdvWaves<E, HS, N, DV>::v;
-  static constexpr bool ok = FP::ok && DP::ok && DkdvCfg<E, HS, N, DV, KVW>::bytes <= 160 * 1024;
+  static constexpr bool KPR = DkdvWaves<E, HS, N, DV>::pair;
+  static constexpr bool ok = FP::ok && DP::ok && DkdvCfg<E, HS, N, DV, KVW, KPR>::bytes <= 160 * 1024;
 };
 
 // forward kernel choice: DTA_FWD_PIPE=1 (env) or -DDTA_FWD_PIPE_DEFAULT=1 selects the
@@ -2435,13 +2468,14 @@ int launch_dkdv_t(const BwdParams& p, hipStream_t st) {
       return (int)hipGetLastError();
     }
   }
-  constexpr int bytes = DkdvCfg<E, HS, N, DV, NW>::bytes;
+  constexpr bool PR = PL::KPR;
+  constexpr int bytes = DkdvCfg<E, HS, N, DV, NW, PR>::bytes;
   dim3 grid((p.T + NW * 32 - 1) / (NW * 32), p.H, p.B);
   dim3 block(NW * 64);
   constexpr bool FUSED = DkdvSplit<HS, N, DV>::fused;
   auto run = [&](auto DKV, auto DVVV, auto SRDV) -> int {
     auto kern = attn_dkdv_kernel<E, HS, N, DV, NW, decltype(DKV)::value, decltype(DVVV)::value, decltype(SRDV)::value,
-                                 DROP>;
+                                 DROP, PR>;
     if (int e = set_smem(kern, bytes)) return e;
     hipLaunchKernelGGL(kern, grid, block, bytes, st, p);
     return 0;
@@ -2455,7 +2489,7 @@ int launch_dkdv_t(const BwdParams& p, hipStream_t st) {
     }
   };
   int e = 0;
-  if constexpr (TileRing<E, HS, N, DV, NW, true>::ok) {
+  if constexpr (TileRing<E, HS, N, DV, NW, true, DkdvCfg<E, HS, N, DV, NW, PR>::BQ>::ok) {
     e = dkdv_mode() != 0 && ring_layout_ok(p, (int)sizeof(E)) ? go(std::true_type{}) : go(std::false_type{});
   } else {
     e = go(std::false_type{});
