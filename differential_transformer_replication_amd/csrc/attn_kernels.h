@@ -45,8 +45,8 @@
 //   DTA_DKDV_STAGGER  waves 4-7 defer their dV product by one step   dK/dV 1.547 -> 1.747 ms (8 VGPR spill)
 //   DTA_FWD_LATE / DTA_DKDV_LATE   next tile's DMA after the compute  fwd 1.038 -> 1.035, dK/dV 1.564 -> 1.554 (noise)
 //   DTA_FWD_SPLIT / DTA_DKDV_SPLIT DMA slots spread over the step     fwd 1.010 -> 1.048, dK/dV 1.541 -> 1.616
-#ifndef DTA_DKDV_BQ          // 64: cfg2 dK/dV 1.543 -> 1.455 ms (one-process A/B)
-#define DTA_DKDV_BQ 64
+#ifndef DTA_DKDV_BQ   // 64: cfg2 8-wave dK/dV 1.543 -> 1.455 ms; superseded by the paired plan (bf16), spills fp16
+#define DTA_DKDV_BQ 32
 #endif
 #ifndef DTA_DKDV_STAGGER
 #define DTA_DKDV_STAGGER 0
@@ -472,11 +472,14 @@ inline bool kv_layout_ok(const P& p, int es) {
 #ifndef DTA_DKDV_PAIR          // 1: cfg2 dK/dV 1.499 -> 1.406 ms (one-process A/B); fwd / dQ: slower, off
 #define DTA_DKDV_PAIR 1
 #endif
-#ifndef DTA_FWD_PAIR
-#define DTA_FWD_PAIR 0
+#ifndef DTA_FWD_PAIR   // 2: fwd 1.004 -> 0.978 ms (branch 0's Q in registers, 64-key tiles); 1 (32-key tiles): slower
+#define DTA_FWD_PAIR 2
 #endif
-#ifndef DTA_DQ_PAIR
-#define DTA_DQ_PAIR 0
+#ifndef DTA_FWD_PAIR_AHEAD     // paired forward: S operand reads ahead of the chain (costs registers)
+#define DTA_FWD_PAIR_AHEAD 0
+#endif
+#ifndef DTA_DQ_PAIR    // 2: dQ 1.115 -> 1.013 ms (same plan); 1 (32-key tiles): slower
+#define DTA_DQ_PAIR 2
 #endif
 constexpr int ring_stages_lim(int fixed_bytes, int tile_bytes, int lim) {
   return (fixed_bytes + 4 * tile_bytes <= lim) ? 4 : (fixed_bytes + 3 * tile_bytes <= lim) ? 3 : 2;
@@ -492,12 +495,13 @@ struct FwdChunk {
   static constexpr int DVC = DV <= cap ? DV : (cap >= 128 && DV % 128 == 0 ? 128 : (cap >= 64 ? 64 : 32));
 };
 
-template <class E, int HS, int N, int DVC, int NW, bool QREG>
+template <class E, int HS, int N, int DVC, int NW, bool QREG, int QRH = 0>
 struct FwdCfg {
+  // QRH > 0 (paired plan): the first QRH branches' Q rows stay in registers
   static constexpr bool PAIR = DTA_FWD_PAIR && NW == 4 && !QREG && sizeof(E) == 2;
-  static constexpr int BN = PAIR ? 32 : FwdTile<E>::BN;
+  static constexpr int BN = (PAIR && QRH == 0) ? 32 : FwdTile<E>::BN;
   static constexpr int BM = NW * 32;
-  static constexpr int nQ = QREG ? 0 : N * BM * HS;
+  static constexpr int nQ = QREG ? 0 : (N - QRH) * BM * HS;
   static constexpr int nK = N * BN * HS;
   static constexpr int nV = BN * DVC;
   static constexpr int NS = ring_stages_lim(nQ * (int)sizeof(E), (nK + nV) * (int)sizeof(E),
@@ -505,11 +509,12 @@ struct FwdCfg {
   static constexpr int bytes = (nQ + NS * nK + NS * nV) * (int)sizeof(E);
   // rough VGPR count (accumulators, two key blocks of scores, P, Q fragments,
   // addresses); a plan that fits 256 keeps the two-waves-per-SIMD bound
-  static constexpr int regs = N * DVC / 2 + N * 2 * 16 + N * 8 + (QREG ? N * HS / 4 : 0) + 48;
+  static constexpr int regs = N * DVC / 2 + N * 2 * 16 + N * 8 + (QREG ? N : QRH) * HS / 4 + 48;
   static constexpr int WPE = regs <= 256 ? 2 : simd_waves(NW, bytes);
 };
 
-template <class E, int HS, int N, int DV = 2 * HS>
+// NP: no paired plan (the dropout instantiations: their extra registers spill it)
+template <class E, int HS, int N, int DV = 2 * HS, bool NP = false>
 struct FwdPick {
   static constexpr int DVC = FwdChunk<N, DV>::DVC;
   static constexpr int LIM = 160 * 1024;
@@ -519,21 +524,28 @@ struct FwdPick {
   static constexpr bool q8 = NWMAX >= 8 && FwdCfg<E, HS, N, DVC, 8, false>::bytes <= LIM &&
                              FwdCfg<E, HS, N, DVC, 8, false>::regs <= 280;
   static constexpr bool q4 = FwdCfg<E, HS, N, DVC, 4, false>::bytes <= LIM;
-  static constexpr bool pair = DTA_FWD_PAIR && q8 && FwdCfg<E, HS, N, DVC, 4, false>::PAIR &&
-                                FwdCfg<E, HS, N, DVC, 4, false>::bytes <= 80 * 1024;
+  // DTA_FWD_PAIR = 2: paired 4-wave plan with 64-key tiles and branch 0's Q in registers
+  static constexpr int QRH = (DTA_FWD_PAIR == 2 && q8 && N >= 2 &&
+                              FwdCfg<E, HS, N, DVC, 4, false, 1>::bytes <= 80 * 1024) ? 1 : 0;
+  static constexpr bool pair = !NP && DTA_FWD_PAIR && (DTA_FWD_PAIR == 1 || QRH == 1) && q8 &&
+                                FwdCfg<E, HS, N, DVC, 4, false, QRH>::PAIR &&
+                                FwdCfg<E, HS, N, DVC, 4, false, QRH>::bytes <= 80 * 1024;
+  static constexpr int QH = pair ? QRH : 0;
   static constexpr int NW = pair ? 4 : (q8 ? 8 : (q4 ? 4 : 4));
   static constexpr bool QREG = !(q8 || q4);
-  static constexpr bool ok = FwdCfg<E, HS, N, DVC, NW, QREG>::bytes <= LIM;
+  static constexpr bool ok = FwdCfg<E, HS, N, DVC, NW, QREG, QH>::bytes <= LIM;
 };
 
-template <class E, int HS, int N, int DVC, int NW, bool QREG, bool SRD, bool DROP>
-__global__ __launch_bounds__(NW * 64, (FwdCfg<E, HS, N, DVC, NW, QREG>::WPE)) void attn_fwd_kernel(FwdParams p) {
+template <class E, int HS, int N, int DVC, int NW, bool QREG, bool SRD, bool DROP, int QRH>
+__global__ __launch_bounds__(NW * 64, (FwdCfg<E, HS, N, DVC, NW, QREG, QRH>::PAIR ? 2 : FwdCfg<E, HS, N, DVC, NW, QREG, QRH>::WPE))
+void attn_fwd_kernel(FwdParams p) {
   using O = Ops<E>;
   using frag = typename O::frag;
   using QI = Img<E, HS>;
   using KI = Img<E, HS>;
   using VI = Img<E, DVC>;
-  using CF = FwdCfg<E, HS, N, DVC, NW, QREG>;
+  using CF = FwdCfg<E, HS, N, DVC, NW, QREG, QRH>;
+  constexpr int NQR = QREG ? N : QRH;      // branches whose Q rows live in registers
   constexpr int BN = CF::BN, BM = CF::BM, NTHR = NW * 64;
   constexpr int KS = O::KSTEP;
   constexpr int NSQ = HS / KS;
@@ -572,18 +584,16 @@ __global__ __launch_bounds__(NW * 64, (FwdCfg<E, HS, N, DVC, NW, QREG>::WPE)) vo
 #pragma unroll
   for (int i = 0; i < N; ++i) coef[i] = p.coef[hh * N + i];
 
-  frag qf[QREG ? N : 1][QREG ? NSQ : 1];
-  if constexpr (QREG) {
+  frag qf[NQR > 0 ? NQR : 1][NQR > 0 ? NSQ : 1];
 #pragma unroll
-    for (int i = 0; i < N; ++i)
+  for (int i = 0; i < NQR; ++i)
 #pragma unroll
-      for (int s = 0; s < NSQ; ++s)
-        qf[i][s] = qrow < T ? O::load_global(gq + (int64_t)qrow * p.q.st + i * p.q.si + s * KS + hf * O::KH)
-                            : O::zero();
-  } else {
+    for (int s = 0; s < NSQ; ++s)
+      qf[i][s] = qrow < T ? O::load_global(gq + (int64_t)qrow * p.q.st + i * p.q.si + s * KS + hf * O::KH)
+                          : O::zero();
 #pragma unroll
-    for (int i = 0; i < N; ++i) stage<E, HS, BM, HS, NTHR>(Qs + i * BM * HS, gq + i * p.q.si, p.q.st, q0, T - 1, tid);
-  }
+  for (int i = NQR; i < N; ++i)
+    stage<E, HS, BM, HS, NTHR>(Qs + (i - NQR) * BM * HS, gq + i * p.q.si, p.q.st, q0, T - 1, tid);
 
   const int kend = min(T, q0 + BM);
   const int ntiles = (kend + BN - 1) / BN;
@@ -735,10 +745,10 @@ __global__ __launch_bounds__(NW * 64, (FwdCfg<E, HS, N, DVC, NW, QREG>::WPE)) vo
         // row operands: byte R*ROWB + (Lrow ^ 32 s) for a 32-row block at row R
         const int Lr = row_lane<KI::ROWB>(lane);
         const char* kbase = reinterpret_cast<const char*>(Ki);
-        const char* qbase = reinterpret_cast<const char*>(Qs + i * BM * HS) + wave * 32 * QI::ROWB;
+        const char* qbase = reinterpret_cast<const char*>(Qs + (i >= NQR ? i - NQR : 0) * BM * HS) + wave * 32 * QI::ROWB;
 #pragma unroll
         for (int kb = 0; kb < NKB; ++kb) sa[i][kb] = f32x16{};
-        if constexpr (NSQ * (NKB + 1) <= 12) {
+        if constexpr (NSQ * (NKB + 1) <= 12 && (QRH == 0 || DTA_FWD_PAIR_AHEAD)) {
           // every operand read of this branch's S^T issued ahead of its MFMA chain,
           // so the chain waits on the LDS latency once instead of per k-step
           // (head sizes <= 64; at 128 the 24 fragments do not fit the registers)
@@ -746,7 +756,7 @@ __global__ __launch_bounds__(NW * 64, (FwdCfg<E, HS, N, DVC, NW, QREG>::WPE)) vo
 #pragma unroll
           for (int s = 0; s < NSQ; ++s) {
             const int o = Lr ^ (32 * s);
-            if constexpr (QREG) qfr[s] = qf[i][s];
+            if (i < NQR) qfr[s] = qf[i < NQR ? i : 0][s];
             else qfr[s] = *reinterpret_cast<const frag*>(qbase + o);
 #pragma unroll
             for (int kb = 0; kb < NKB; ++kb) kfr[kb][s] = *reinterpret_cast<const frag*>(kbase + kb * 32 * KI::ROWB + o);
@@ -755,14 +765,15 @@ __global__ __launch_bounds__(NW * 64, (FwdCfg<E, HS, N, DVC, NW, QREG>::WPE)) vo
           for (int s = 0; s < NSQ; ++s)
 #pragma unroll
             for (int kb = 0; kb < NKB; ++kb) sa[i][kb] = O::mma(kfr[kb][s], qfr[s], sa[i][kb]);
-          __builtin_amdgcn_sched_group_barrier(0x100, NSQ * (NKB + (QREG ? 0 : 1)), 0);
+          if (i < NQR) __builtin_amdgcn_sched_group_barrier(0x100, NSQ * NKB, 0);
+          else __builtin_amdgcn_sched_group_barrier(0x100, NSQ * (NKB + 1), 0);
           __builtin_amdgcn_sched_group_barrier(0x008, NSQ * NKB, 0);
         } else {
 #pragma unroll
           for (int s = 0; s < NSQ; ++s) {
             const int o = Lr ^ (32 * s);
             frag qb;
-            if constexpr (QREG) qb = qf[i][s];
+            if (i < NQR) qb = qf[i < NQR ? i : 0][s];
             else qb = *reinterpret_cast<const frag*>(qbase + o);
 #pragma unroll
             for (int kb = 0; kb < NKB; ++kb)
@@ -776,8 +787,8 @@ __global__ __launch_bounds__(NW * 64, (FwdCfg<E, HS, N, DVC, NW, QREG>::WPE)) vo
 #pragma unroll
           for (int s = 0; s < NSQ; ++s) {
             frag qb;
-            if constexpr (QREG) qb = qf[i][s];
-            else qb = QI::row(Qs + i * BM * HS, wave * 32 + c32, s, hf);
+            if (i < NQR) qb = qf[i < NQR ? i : 0][s];
+            else qb = QI::row(Qs + (i >= NQR ? i - NQR : 0) * BM * HS, wave * 32 + c32, s, hf);
             sa[i][kb] = O::mma(KI::row(Ki, kb * 32 + c32, s, hf), qb, sa[i][kb]);
           }
         }
@@ -1243,13 +1254,15 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_pipe_kernel(FwdParams p) {
 }
 
 // ------------------------------------------------------ backward: dQ ---
-template <class E, int HS, int N, int DV, int NW, bool QREG>
+template <class E, int HS, int N, int DV, int NW, bool QREG, int QRH = 0>
 struct DqCfg {
+  // QRH > 0 (paired plan): the first QRH branches' Q rows stay in registers, the
+  // rest in LDS, so Q plus a 2-stage ring of 64-key tiles fits 80 KB
   static constexpr bool PAIR = DTA_DQ_PAIR && NW == 4 && !QREG && sizeof(E) == 2;
-  static constexpr int BN = PAIR ? 32 : FwdTile<E>::BN;
+  static constexpr int BN = (PAIR && QRH == 0) ? 32 : FwdTile<E>::BN;
   static constexpr int BM = NW * 32;
   static constexpr int HSP = HS < 32 ? 32 : HS;
-  static constexpr int nQ = QREG ? 0 : N * BM * HS;
+  static constexpr int nQ = QREG ? 0 : (N - QRH) * BM * HS;
   static constexpr int nK = N * BN * HSP;
   static constexpr int nV = BN * DV;
   static constexpr int NS = ring_stages_lim(nQ * (int)sizeof(E), (nK + nV) * (int)sizeof(E),
@@ -1257,22 +1270,29 @@ struct DqCfg {
   static constexpr int bytes = (nQ + NS * nK + NS * nV) * (int)sizeof(E);
 };
 
-template <class E, int HS, int N, int DV = 2 * HS>
+template <class E, int HS, int N, int DV = 2 * HS, bool NP = false>
 struct DqPick {
   static constexpr int LIM = 160 * 1024;
   static constexpr bool q8 = sizeof(E) == 2 && DqCfg<E, HS, N, DV, 8, false>::bytes <= LIM;
-  static constexpr bool pair = DTA_DQ_PAIR && q8 && DqCfg<E, HS, N, DV, 4, false>::bytes <= 80 * 1024;
+  // DTA_DQ_PAIR = 2: paired 4-wave plan with 64-key tiles and branch 0's Q in registers
+  static constexpr int QRH = (DTA_DQ_PAIR == 2 && q8 && N >= 2 &&
+                              DqCfg<E, HS, N, DV, 4, false, 1>::bytes <= 80 * 1024) ? 1 : 0;
+  // (head size >= 64: the hs = 32, N = 3 paired plan spills)
+  static constexpr bool pair = !NP && DTA_DQ_PAIR && (DTA_DQ_PAIR == 1 || QRH == 1) && q8 && HS >= 64 &&
+                               DqCfg<E, HS, N, DV, 4, false, QRH>::bytes <= 80 * 1024;
   static constexpr int NW = pair ? 4 : (q8 ? 8 : (sizeof(E) == 2 ? 4 : 2));
   static constexpr bool QREG = pair ? false : !q8;
-  static constexpr bool ok = DqCfg<E, HS, N, DV, NW, QREG>::bytes <= LIM;
+  static constexpr int QH = pair ? QRH : 0;
+  static constexpr bool ok = DqCfg<E, HS, N, DV, NW, QREG, QH>::bytes <= LIM;
 };
 
-template <class E, int HS, int N, int DV, int NW, bool QREG, bool OUTF32, bool SRD, bool DROP>
-__global__ __launch_bounds__(NW * 64, simd_waves(NW, DqCfg<E, HS, N, DV, NW, QREG>::bytes))
+template <class E, int HS, int N, int DV, int NW, bool QREG, bool OUTF32, bool SRD, bool DROP, int QRH>
+__global__ __launch_bounds__(NW * 64, simd_waves(NW, DqCfg<E, HS, N, DV, NW, QREG, QRH>::bytes))
 void attn_dq_kernel(BwdParams p) {
   using O = Ops<E>;
   using frag = typename O::frag;
-  using CF = DqCfg<E, HS, N, DV, NW, QREG>;
+  using CF = DqCfg<E, HS, N, DV, NW, QREG, QRH>;
+  constexpr int NQR = QREG ? N : QRH;      // branches whose Q rows live in registers
   using QI = Img<E, HS>;
   constexpr int HSP = CF::HSP;
   using KI = Img<E, HSP>;
@@ -1326,7 +1346,7 @@ void attn_dq_kernel(BwdParams p) {
   };
 
   // ---- per-row operands in registers: Q_i and dO rows (B operands), LSE, delta
-  frag qf[QREG ? N : 1][QREG ? NSQ : 1], df[NSV];
+  frag qf[NQR > 0 ? NQR : 1][NQR > 0 ? NSQ : 1], df[NSV];
   float coef[N], lse[N], del[N];
   const int64_t rs = (((int64_t)0 * p.B + b) * p.H + hh) * T + qrow;     // [i][b][h][t], i = 0
   const int64_t bstride = (int64_t)p.B * p.H * T;
@@ -1336,11 +1356,11 @@ void attn_dq_kernel(BwdParams p) {
 #pragma unroll
   for (int i = 0; i < N; ++i) {
     coef[i] = p.coef[hh * N + i];
-    if constexpr (QREG) {
+    if (i < NQR) {
 #pragma unroll
       for (int s = 0; s < NSQ; ++s)
-        qf[i][s] = rowok ? O::load_global(gq + (int64_t)qrow * p.q.st + i * p.q.si + s * KS + hf * O::KH)
-                         : O::zero();
+        qf[i < NQR ? i : 0][s] = rowok ? O::load_global(gq + (int64_t)qrow * p.q.st + i * p.q.si + s * KS + hf * O::KH)
+                                       : O::zero();
     }
     lse[i] = rowok ? p.lse[rs + i * bstride] : 0.f;
     // delta_i = <dO, O_i> over this row (flash-backward preprocess), both lane halves
@@ -1374,7 +1394,8 @@ void attn_dq_kernel(BwdParams p) {
 
   if constexpr (!QREG) {
 #pragma unroll
-    for (int i = 0; i < N; ++i) stage<E, HS, BM, HS, NTHR>(Qs + i * BM * HS, gq + i * p.q.si, p.q.st, q0, T - 1, tid);
+    for (int i = NQR; i < N; ++i)
+      stage<E, HS, BM, HS, NTHR>(Qs + (i - NQR) * BM * HS, gq + i * p.q.si, p.q.st, q0, T - 1, tid);
   }
   const int tile_pieces = SRD ? KR::pieces(wave)
                               : N * stage_pieces<E, HSP, BN, HS, NW>(wave) + stage_pieces<E, DV, BN, DV, NW>(wave);
@@ -1435,7 +1456,8 @@ void attn_dq_kernel(BwdParams p) {
           if constexpr (sizeof(E) == 2) {
             const int Lr = row_lane<KI::ROWB>(lane);
             const char* kbase = reinterpret_cast<const char*>(Ki);
-            const char* qbase = reinterpret_cast<const char*>(Qs + i * BM * HS) + wave * 32 * QI::ROWB;
+            const char* qbase = reinterpret_cast<const char*>(Qs + (i >= NQR ? i - NQR : 0) * BM * HS) +
+                                wave * 32 * QI::ROWB;
             const int Lq = row_lane<QI::ROWB>(lane);
 #pragma unroll
             for (int kb = 0; kb < NKB; ++kb) sa[kb] = f32x16{};
@@ -1444,7 +1466,7 @@ void attn_dq_kernel(BwdParams p) {
               frag kfr[NKB][NSQ], qfr[NSQ];
 #pragma unroll
               for (int s = 0; s < NSQ; ++s) {
-                if constexpr (QREG) qfr[s] = qf[i][s];
+                if (i < NQR) qfr[s] = qf[i < NQR ? i : 0][s];
                 else qfr[s] = *reinterpret_cast<const frag*>(qbase + (Lq ^ (32 * s)));
 #pragma unroll
                 for (int kb = 0; kb < NKB; ++kb)
@@ -1454,13 +1476,14 @@ void attn_dq_kernel(BwdParams p) {
               for (int s = 0; s < NSQ; ++s)
 #pragma unroll
                 for (int kb = 0; kb < NKB; ++kb) sa[kb] = O::mma(kfr[kb][s], qfr[s], sa[kb]);
-              __builtin_amdgcn_sched_group_barrier(0x100, NSQ * (NKB + (QREG ? 0 : 1)), 0);
+              if (i < NQR) __builtin_amdgcn_sched_group_barrier(0x100, NSQ * NKB, 0);
+              else __builtin_amdgcn_sched_group_barrier(0x100, NSQ * (NKB + 1), 0);
               __builtin_amdgcn_sched_group_barrier(0x008, NSQ * NKB, 0);
             } else {
 #pragma unroll
             for (int s = 0; s < NSQ; ++s) {
               frag qb;
-              if constexpr (QREG) qb = qf[i][s];
+              if (i < NQR) qb = qf[i < NQR ? i : 0][s];
               else qb = *reinterpret_cast<const frag*>(qbase + (Lq ^ (32 * s)));
 #pragma unroll
               for (int kb = 0; kb < NKB; ++kb)
@@ -1474,8 +1497,8 @@ void attn_dq_kernel(BwdParams p) {
 #pragma unroll
               for (int s = 0; s < NSQ; ++s) {
                 frag qb;
-                if constexpr (QREG) qb = qf[i][s];
-                else qb = QI::row(Qs + i * BM * HS, wave * 32 + c32, s, hf);
+                if (i < NQR) qb = qf[i < NQR ? i : 0][s];
+                else qb = QI::row(Qs + (i >= NQR ? i - NQR : 0) * BM * HS, wave * 32 + c32, s, hf);
                 sa[kb] = O::mma(KI::row(Ki, kb * 32 + c32, s, hf), qb, sa[kb]);
               }
             }
@@ -1697,7 +1720,7 @@ struct DkdvSplit {
 // widest key block (waves x 32 keys) whose K rows plus a 2+-stage query ring fit
 // LDS; 8 waves (two per SIMD, 256 registers each) only while the rough register
 // count of a launch (dK / dV accumulators, V fragments, scores) fits them
-template <class E, int HS, int N, int DV>
+template <class E, int HS, int N, int DV, bool NP = false>
 struct DkdvWaves {
   static constexpr int LIM = 160 * 1024;
   static constexpr int HSP = HS < 32 ? 32 : HS;
@@ -1707,7 +1730,7 @@ struct DkdvWaves {
                           : DkdvCfg<E, HS, N, DV, 4>::bytes <= LIM ? 4 : 2;
   // DTA_DKDV_PAIR (default): where the 8-wave plan applies, two 4-wave workgroups per CU instead
   // (bf16 only: the fp16 paired instantiation spills 16 VGPRs)
-  static constexpr bool pair = DTA_DKDV_PAIR && std::is_same<E, __bf16>::value && v8 == 8 &&
+  static constexpr bool pair = !NP && DTA_DKDV_PAIR && std::is_same<E, __bf16>::value && v8 == 8 &&
                                DkdvCfg<E, HS, N, DV, 4, true>::bytes <= 80 * 1024;
   static constexpr int v = pair ? 4 : v8;
 };
@@ -2404,7 +2427,7 @@ inline bool fwd_pipe() {
 template <class E, int HS, int N, int DV_, bool DROP>
 int launch_fwd_t(const FwdParams& p, hipStream_t st) {
   using PL = Plan<E, HS, N, DV_>;
-  using FP = typename PL::FP;
+  using FP = FwdPick<E, HS, N, PL::DV, DROP>;
   constexpr int DVC = FP::DVC, NW = FP::NW;
   if constexpr (!DROP && FwdPipeCfg<E, HS, N, DVC>::ok) {
     if (fwd_pipe() && kv_layout_ok(p, (int)sizeof(E))) {
@@ -2415,16 +2438,17 @@ int launch_fwd_t(const FwdParams& p, hipStream_t st) {
       return (int)hipGetLastError();
     }
   }
-  constexpr int bytes = FwdCfg<E, HS, N, DVC, NW, FP::QREG>::bytes;
+  constexpr int QH = FP::QH;
+  constexpr int bytes = FwdCfg<E, HS, N, DVC, NW, FP::QREG, QH>::bytes;
   dim3 grid((p.T + NW * 32 - 1) / (NW * 32), p.H * (PL::DV / DVC), p.B);
   auto run = [&](auto SRDV) -> int {
-    auto kern = attn_fwd_kernel<E, HS, N, DVC, NW, FP::QREG, decltype(SRDV)::value, DROP>;
+    auto kern = attn_fwd_kernel<E, HS, N, DVC, NW, FP::QREG, decltype(SRDV)::value, DROP, QH>;
     if (int e = set_smem(kern, bytes)) return e;
     hipLaunchKernelGGL(kern, grid, dim3(NW * 64), bytes, st, p);
     return 0;
   };
   int e = 0;
-  if constexpr (KvRing<E, HS, N, DVC, FwdCfg<E, HS, N, DVC, NW, FP::QREG>::BN, NW>::ok)
+  if constexpr (KvRing<E, HS, N, DVC, FwdCfg<E, HS, N, DVC, NW, FP::QREG, QH>::BN, NW>::ok)
     e = kv_staging() && kv_layout_ok(p, (int)sizeof(E)) ? run(std::true_type{}) : run(std::false_type{});
   else
     e = run(std::false_type{});
@@ -2435,19 +2459,21 @@ int launch_fwd_t(const FwdParams& p, hipStream_t st) {
 template <class E, int HS, int N, int DV_, bool DROP>
 int launch_dq_t(const BwdParams& p, hipStream_t st) {
   using PL = Plan<E, HS, N, DV_>;
-  constexpr int NW = PL::DP::NW, DV = PL::DV;
-  constexpr bool QR = PL::DP::QREG;
-  constexpr int bytes = DqCfg<E, HS, N, DV, NW, QR>::bytes;
+  using DP = DqPick<E, HS, N, PL::DV, DROP>;
+  constexpr int NW = DP::NW, DV = PL::DV;
+  constexpr bool QR = DP::QREG;
+  constexpr int QH = DP::QH;
+  constexpr int bytes = DqCfg<E, HS, N, DV, NW, QR, QH>::bytes;
   dim3 grid((p.T + NW * 32 - 1) / (NW * 32), p.H, p.B);
   auto run = [&](auto F32, auto SRDV) -> int {
-    auto kern = attn_dq_kernel<E, HS, N, DV, NW, QR, decltype(F32)::value, decltype(SRDV)::value, DROP>;
+    auto kern = attn_dq_kernel<E, HS, N, DV, NW, QR, decltype(F32)::value, decltype(SRDV)::value, DROP, QH>;
     if (int e = set_smem(kern, bytes)) return e;
     hipLaunchKernelGGL(kern, grid, dim3(NW * 64), bytes, st, p);
     return 0;
   };
   auto go = [&](auto SRDV) -> int { return p.dq32 ? run(std::true_type{}, SRDV) : run(std::false_type{}, SRDV); };
   int e = 0;
-  if constexpr (KvRing<E, HS, N, DV, DqCfg<E, HS, N, DV, NW, QR>::BN, NW>::ok && DqCfg<E, HS, N, DV, NW, QR>::HSP == HS)
+  if constexpr (KvRing<E, HS, N, DV, DqCfg<E, HS, N, DV, NW, QR, QH>::BN, NW>::ok && DqCfg<E, HS, N, DV, NW, QR, QH>::HSP == HS)
     e = kv_staging() && kv_layout_ok(p, (int)sizeof(E)) ? go(std::true_type{}) : go(std::false_type{});
   else
     e = go(std::false_type{});
@@ -2458,7 +2484,8 @@ int launch_dq_t(const BwdParams& p, hipStream_t st) {
 template <class E, int HS, int N, int DV_, bool DROP>
 int launch_dkdv_t(const BwdParams& p, hipStream_t st) {
   using PL = Plan<E, HS, N, DV_>;
-  constexpr int NW = PL::KVW, DV = PL::DV;
+  using KW = DkdvWaves<E, HS, N, PL::DV, DROP>;
+  constexpr int NW = KW::v, DV = PL::DV;
   if constexpr (!DROP && Dkdv4Cfg<E, HS, N, DV>::ok) {
     if (dkdv_mode() == 4 && ring_layout_ok(p, (int)sizeof(E))) {
       using C4 = Dkdv4Cfg<E, HS, N, DV>;
@@ -2468,7 +2495,7 @@ int launch_dkdv_t(const BwdParams& p, hipStream_t st) {
       return (int)hipGetLastError();
     }
   }
-  constexpr bool PR = PL::KPR;
+  constexpr bool PR = KW::pair;
   constexpr int bytes = DkdvCfg<E, HS, N, DV, NW, PR>::bytes;
   dim3 grid((p.T + NW * 32 - 1) / (NW * 32), p.H, p.B);
   dim3 block(NW * 64);
