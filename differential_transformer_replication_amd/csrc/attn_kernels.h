@@ -295,6 +295,20 @@ __device__ __forceinline__ void stage(E* img, const E* g, int64_t rs, int row0, 
   }
 }
 
+// Multiply n elements of an LDS array by s in place (16 bytes per lane and step; n
+// a multiple of 16 / sizeof(E)).  Every thread of the block calls it between barriers.
+template <class E, int NTHR>
+__device__ __forceinline__ void scale_lds(E* a, int n, float s, int tid) {
+  constexpr int V = 16 / (int)sizeof(E);
+  typedef E vec __attribute__((ext_vector_type(V)));
+  for (int e = tid * V; e < n; e += NTHR * V) {
+    vec x = *reinterpret_cast<vec*>(a + e);
+#pragma unroll
+    for (int j = 0; j < V; ++j) x[j] = (E)((float)x[j] * s);
+    *reinterpret_cast<vec*>(a + e) = x;
+  }
+}
+
 // Per-row fp32 vectors (LSE / delta) of NR rows x N branches by 4-byte LDS-DMA.
 // src layout [i][b][h][t]: branch stride bs; dst [i][NR] (padded to 64-float pieces).
 template <int N, int NR, int NTHR>
@@ -1379,7 +1393,10 @@ void attn_dq_kernel(BwdParams p) {
     }
     d = wave_sum_halves(d);
     del[i] = d;
-    if (rowok && hf == 0) p.delta[rs + i * bstride] = coef[i] * d;     // c_i * delta_i for attn_dkdv
+    // row constants for attn_dkdv, which folds c_i into its dK_i epilogue: without
+    // dropout -delta_0 (its dP accumulator's seed) and delta_0 - delta_i (i >= 1);
+    // with dropout delta_i
+    if (rowok && hf == 0) p.delta[rs + i * bstride] = DROP ? d : (i == 0 ? -d : del[0] - d);
     // d(coef)[h][i] = sum over rows of delta_i: one atomic per wave
     float w = (rowok && hf == 0) ? d : 0.f;
 #pragma unroll
@@ -1845,6 +1862,10 @@ void attn_dkdv_kernel(BwdParams p) {
     if (j < ntiles) stage_q(kb0 + j * BQ, j);
   wait_vm(tile_pieces * max(0, min(LA, ntiles) - 1));
   lds_barrier();
+  // K_i rows scaled once by scale*log2e in place, so S'_i = Q_i (sl2 K_i)^T; the S
+  // accumulators start at the tile's -LSE rows and P = exp2(S'_i) needs no fma
+  scale_lds<E, NTHR>(Ks, CF::nK, p.sl2, tid);
+  lds_barrier();
   const bool wave_keys = kw0 < T;
   // dV += (sum_i c_i P_i)^T dO of one tile from its packed P sums
   auto dv_update = [&](const frag& p0, const frag& p1, const E* Dc) {
@@ -1933,7 +1954,18 @@ void attn_dkdv_kernel(BwdParams p) {
       const float* Lc = (SRD ? reinterpret_cast<const float*>(sg + RG::OFF_L) : Lb + buf * NP) + so;
       const float* Gc = (SRD ? reinterpret_cast<const float*>(sg + RG::OFF_G) : Gb + buf * NP) + so;
       {
+      // Gc rows (attn_dq): without dropout -delta_0 | delta_0 - delta_i, and the dP
+      // accumulator starts at -delta_0, so dS_0 / c_0 = P_0 dpa and dS_i / c_i =
+      // P_i (dpa + delta_0 - delta_i); with dropout delta_i and an unseeded dP
       f32x16 dpa = f32x16{};
+      if constexpr (DK && !DROP) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 g4 = *reinterpret_cast<const f32x4*>(Gc + 8 * g + 4 * hf);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) dpa[4 * g + j] = g4[j];
+        }
+      }
       if constexpr (DK) {
         if constexpr (sizeof(E) == 2) {
           const int Ld = row_lane<DI::ROWB>(lane);
@@ -1952,7 +1984,14 @@ void attn_dkdv_kernel(BwdParams p) {
       const int lim_hi = T - 1 - qs - 4 * hf;         // masked if rowof_c > lim_hi (query >= T)
 #pragma unroll
       for (int i = 0; i < N; ++i) {
-        f32x16 sa = f32x16{};
+        // S'_i accumulator seeded with the -LSE rows (K_i is pre-scaled by sl2)
+        f32x16 sa;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 l4 = *reinterpret_cast<const f32x4*>(Lc + i * BQ + 8 * g + 4 * hf);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) sa[4 * g + j] = l4[j];
+        }
         const E* Qi = Qc + i * BQ * HSP;
         if constexpr (sizeof(E) == 2) {
           const int Lq = row_lane<QI::ROWB>(lane), Lk = row_lane<KI::ROWB>(lane);
@@ -1975,26 +2014,29 @@ void attn_dkdv_kernel(BwdParams p) {
             sa = O::mma(QI::row(Qi, c32, s, hf), KI::row(Ks + i * BK * HS, wave * 32 + c32, s, hf), sa);
         }
         if constexpr (SPLIT) if (i == 0) issue_part(U1{}, U2{});
-        // sa[r] = S_i[q0 + rowof(r)][krow]; rows 4g..4g+3 of a lane are consecutive.
-        // Gc holds c_i * delta_i (written by attn_dq): dS = P * (c_i dP - c_i delta_i)
+        // sa[r] = S'_i[q0 + rowof(r)][krow] - LSE; rows 4g..4g+3 of a lane are consecutive
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          const f32x4 l4 = *reinterpret_cast<const f32x4*>(Lc + i * BQ + 8 * g + 4 * hf);
           f32x4 d4 = f32x4{};
-          if constexpr (DK) d4 = *reinterpret_cast<const f32x4*>(Gc + i * BQ + 8 * g + 4 * hf);
+          if constexpr (DK) if (DROP || i > 0) d4 = *reinterpret_cast<const f32x4*>(Gc + i * BQ + 8 * g + 4 * hf);
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const int r = 4 * g + j;
-            float arg = fmaf(sa[r], p.sl2, l4[j]);      // l4 = -LSE
+            float arg = sa[r];
             if constexpr (MASK) {
               const int rc = (r & 3) + 8 * (r >> 2);
               arg = (rc < lim_lo || rc > lim_hi) ? -INFINITY : arg;
             }
             const float pr = exp2_fast(arg);
-            float cm = coef[i];                 // dropout: this map element's kept weight c_i * mask/(1-p)
-            if constexpr (DROP) cm *= drop_mul(dkey[i], qs + (r & 3) + 8 * (r >> 2) + 4 * hf, krow, p.drop_thr, p.drop_scale);
-            if constexpr (DVV) pc[r] = fmaf(cm, pr, pc[r]);
-            if constexpr (DK) sa[r] = pr * fmaf(cm, dpa[r], -d4[j]);
+            if constexpr (DROP) {
+              // this map element's kept weight mask/(1-p)
+              const float mk = drop_mul(dkey[i], qs + (r & 3) + 8 * (r >> 2) + 4 * hf, krow, p.drop_thr, p.drop_scale);
+              if constexpr (DVV) pc[r] = fmaf(coef[i] * mk, pr, pc[r]);
+              if constexpr (DK) sa[r] = pr * fmaf(mk, dpa[r], -d4[j]);
+            } else {
+              if constexpr (DVV) pc[r] = i == 0 ? coef[0] * pr : fmaf(coef[i], pr, pc[r]);
+              if constexpr (DK) sa[r] = i == 0 ? pr * dpa[r] : pr * (dpa[r] + d4[j]);
+            }
           }
         }
         if constexpr (DK) {
@@ -2083,19 +2125,21 @@ void attn_dkdv_kernel(BwdParams p) {
   if constexpr (DK) {
     E* gdk = reinterpret_cast<E*>(p.dk.p) + b * p.dk.sb + (int64_t)krow * p.dk.st + hh * p.dk.sh;
 #pragma unroll
-    for (int i = 0; i < N; ++i)
+    for (int i = 0; i < N; ++i) {
+      const float sc = p.scale * coef[i];      // dS_i was accumulated without its c_i
 #pragma unroll
       for (int d = 0; d < NHB; ++d)
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int e = d * 32 + 8 * g + 4 * hf;
           if (e < HS) {
-            float a0 = dk[i][d][4 * g] * p.scale, a1 = dk[i][d][4 * g + 1] * p.scale;
-            float a2 = dk[i][d][4 * g + 2] * p.scale, a3 = dk[i][d][4 * g + 3] * p.scale;
+            float a0 = dk[i][d][4 * g] * sc, a1 = dk[i][d][4 * g + 1] * sc;
+            float a2 = dk[i][d][4 * g + 2] * sc, a3 = dk[i][d][4 * g + 3] * sc;
             if (p.rope) rope_inv4(p.rope, krow, HS, e, a0, a1, a2, a3);
             store4<E>(gdk + i * p.dk.si + e, a0, a1, a2, a3);
           }
         }
+    }
   }
   if constexpr (DVV) {
     E* gdv = reinterpret_cast<E*>(p.dv.p) + b * p.dv.sb + (int64_t)krow * p.dv.st + hh * p.dv.sh;
@@ -2272,14 +2316,20 @@ __global__ __launch_bounds__(256, 1) void attn_dkdv4_kernel(BwdParams p) {
         for (int i = 0; i < N; ++i)
 #pragma unroll
           for (int s = 0; s < NSQ; ++s) sa[u][i] = O::mma(qr[i][s], kf[i][s], sa[u][i]);
-        dpa[u] = f32x16{};
+        // dP accumulator seeded with -delta_0 (attn_dq's row constants, see attn_dkdv_kernel)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 g4 = *reinterpret_cast<const f32x4*>(st0 + OFF_G + (32 * u) * 4 + 32 * g + lrow);
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) dpa[u][4 * g + jj] = g4[jj];
+        }
 #pragma unroll
         for (int s = 0; s < NSV; ++s) dpa[u] = O::mma(dr[s], vf[s], dpa[u]);
 #pragma unroll
         for (int i = 0; i < N; ++i) asm volatile("" : "+v"(sa[u][i]));
         asm volatile("" : "+v"(dpa[u]));
       }
-      // ---- softmax side per sub-tile: P_i = exp2(S'_i); pc = sum_i c_i P_i; dS_i = P_i (c_i dP - c_i delta_i)
+      // ---- softmax side per sub-tile: P_i = exp2(S'_i); pc = sum_i c_i P_i; dS_i / c_i = P_i (dP - delta_i)
       frag pk[2][2], ds[2][N][2];
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
@@ -2290,7 +2340,8 @@ __global__ __launch_bounds__(256, 1) void attn_dkdv4_kernel(BwdParams p) {
         for (int i = 0; i < N; ++i) {
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
-            const f32x4 d4 = *reinterpret_cast<const f32x4*>(st0 + OFF_G + (i * BQ + 32 * u) * 4 + 32 * g + lrow);
+            f32x4 d4 = f32x4{};
+            if (i > 0) d4 = *reinterpret_cast<const f32x4*>(st0 + OFF_G + (i * BQ + 32 * u) * 4 + 32 * g + lrow);
 #pragma unroll
             for (int jj = 0; jj < 4; ++jj) {
               const int r = 4 * g + jj;
@@ -2300,7 +2351,7 @@ __global__ __launch_bounds__(256, 1) void attn_dkdv4_kernel(BwdParams p) {
                 pr = (rc < lim_lo || rc > lim_hi) ? 0.f : pr;
               }
               pc[r] = i == 0 ? coef[0] * pr : fmaf(coef[i], pr, pc[r]);
-              sa[u][i][r] = pr * fmaf(coef[i], dpa[u][r], -d4[jj]);
+              sa[u][i][r] = i == 0 ? pr * dpa[u][r] : pr * (dpa[u][r] + d4[jj]);   // dS_i / c_i
             }
           }
           ds[u][i][0] = O::template pack<0>(sa[u][i]);
@@ -2357,8 +2408,9 @@ __global__ __launch_bounds__(256, 1) void attn_dkdv4_kernel(BwdParams p) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int e = d * 32 + 8 * g + 4 * hf;
-        float a0 = dk[i][d][4 * g] * p.scale, a1 = dk[i][d][4 * g + 1] * p.scale;
-        float a2 = dk[i][d][4 * g + 2] * p.scale, a3 = dk[i][d][4 * g + 3] * p.scale;
+        const float sc = p.scale * coef[i];
+        float a0 = dk[i][d][4 * g] * sc, a1 = dk[i][d][4 * g + 1] * sc;
+        float a2 = dk[i][d][4 * g + 2] * sc, a3 = dk[i][d][4 * g + 3] * sc;
         if (p.rope) rope_inv4(p.rope, krow, HS, e, a0, a1, a2, a3);
         store4<E>(gdk + i * p.dk.si + e, a0, a1, a2, a3);
       }
