@@ -48,6 +48,9 @@
 #ifndef DTA_DKDV_BQ   // 64: cfg2 8-wave dK/dV 1.543 -> 1.455 ms; superseded by the paired plan (bf16), spills fp16
 #define DTA_DKDV_BQ 32
 #endif
+#ifndef DTA_DKDV_LBASE   // dK/dV: per-lane LDS read bases kept in registers across the loop
+#define DTA_DKDV_LBASE 1
+#endif
 #ifndef DTA_DKDV_STAGGER
 #define DTA_DKDV_STAGGER 0
 #endif
@@ -1901,11 +1904,27 @@ void attn_dkdv_kernel(BwdParams p) {
   // is one straight-line body (both variants behind a branch spill).  Lanes with
   // key >= T only pollute their own (never stored) dK/dV columns.
   Stamps st;
+  // per-lane LDS read bases, one register each across the loop (DTA_DKDV_LBASE): every
+  // read of a step is then one v_xad (base ^ k-step) + stage; without the switch they
+  // are re-derived from the lane id each step
+  int LrD = 0, LrQ = 0, LrK = 0, LtQ = 0, LtD = 0;
+  if constexpr (sizeof(E) == 2) {
+    LrD = row_lane<DI::ROWB>(lane); LrQ = row_lane<QI::ROWB>(lane); LrK = row_lane<KI::ROWB>(lane);
+    LtQ = tr_lane<QI::ROWB>(lane); LtD = tr_lane<DI::ROWB>(lane);
+  }
   auto step = [&](int t, auto MASKED) {
     constexpr bool MASK = decltype(MASKED)::value;
     // keep lane-derived addresses loop-variant: recomputed per tile instead of
     // hoisted into (spilled) registers across the whole loop
     asm volatile("" : "+v"(lane));
+    if constexpr (DTA_DKDV_LBASE && sizeof(E) == 2) {
+      asm volatile("" : "+v"(LrD), "+v"(LrQ), "+v"(LtQ), "+v"(LtD));
+      if constexpr (QI::ROWB == KI::ROWB) LrK = LrQ;     // same row pitch (HS >= 32)
+      else asm volatile("" : "+v"(LrK));
+    } else if constexpr (sizeof(E) == 2) {
+      LrD = row_lane<DI::ROWB>(lane); LrQ = row_lane<QI::ROWB>(lane); LrK = row_lane<KI::ROWB>(lane);
+      LtQ = tr_lane<QI::ROWB>(lane); LtD = tr_lane<DI::ROWB>(lane);
+    }
     tid = (wave << 6) + lane; hf = lane >> 5; c32 = lane & 31;
     krow = kw0 + c32;
     const int buf = t % NS;
@@ -1968,7 +1987,7 @@ void attn_dkdv_kernel(BwdParams p) {
       }
       if constexpr (DK) {
         if constexpr (sizeof(E) == 2) {
-          const int Ld = row_lane<DI::ROWB>(lane);
+          const int Ld = LrD;
           const char* dbase = reinterpret_cast<const char*>(Dc);
 #pragma unroll
           for (int s = 0; s < NSV; ++s) dpa = O::mma(*reinterpret_cast<const frag*>(dbase + (Ld ^ (32 * s))), vf[s], dpa);
@@ -1994,7 +2013,7 @@ void attn_dkdv_kernel(BwdParams p) {
         }
         const E* Qi = Qc + i * BQ * HSP;
         if constexpr (sizeof(E) == 2) {
-          const int Lq = row_lane<QI::ROWB>(lane), Lk = row_lane<KI::ROWB>(lane);
+          const int Lq = LrQ, Lk = LrK;
           const char* qbase = reinterpret_cast<const char*>(Qi);
           const char* kbase = reinterpret_cast<const char*>(Ks + i * BK * HS) + wave * 32 * KI::ROWB;
           // operand reads of this branch's S ahead of its MFMA chain (see attn_fwd_kernel)
@@ -2042,7 +2061,7 @@ void attn_dkdv_kernel(BwdParams p) {
         if constexpr (DK) {
           if constexpr (sizeof(E) == 2) {
             const unsigned qb = lds_addr(Qi);
-            const int Lq = tr_lane<QI::ROWB>(lane);
+            const int Lq = LtQ;
             lds64 r[NHB][4];
             sfor<NHB>([&](auto D) {
               constexpr int d = decltype(D)::value;
@@ -2076,7 +2095,7 @@ void attn_dkdv_kernel(BwdParams p) {
       } else if constexpr (DVV) {
         if constexpr (sizeof(E) == 2) {
           const unsigned db = lds_addr(Dc);
-          const int Ld = tr_lane<DI::ROWB>(lane);
+          const int Ld = LtD;
           const frag p0 = O::template pack<0>(pc), p1 = O::template pack<1>(pc);
           constexpr int NP2 = NVB >= 2 ? 2 : 1;       // d-blocks per LDS read batch
           sfor<NVB / NP2>([&](auto D2) {
