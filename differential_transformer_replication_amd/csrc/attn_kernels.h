@@ -48,6 +48,12 @@
 #ifndef DTA_DKDV_BQ   // 64: cfg2 8-wave dK/dV 1.543 -> 1.455 ms; superseded by the paired plan (bf16), spills fp16
 #define DTA_DKDV_BQ 32
 #endif
+#ifndef DTA_FWD_LBASE    // forward: per-lane LDS read bases kept in registers across the loop
+#define DTA_FWD_LBASE 1
+#endif
+#ifndef DTA_DQ_LBASE     // dQ: per-lane LDS read bases kept in registers across the loop
+#define DTA_DQ_LBASE 0   // measured +2% on dQ at cfg2 (253 VGPRs): off
+#endif
 #ifndef DTA_DKDV_LBASE   // dK/dV: per-lane LDS read bases kept in registers across the loop
 #define DTA_DKDV_LBASE 1
 #endif
@@ -235,15 +241,26 @@ __device__ __forceinline__ int row_lane(int lane) {
 
 typedef long long lds64;
 // two fragments (k-steps s = 0, 1) of a 32x32 transposed operand block
-template <int ROWB, int RB>
+template <int ROWB, int RB, int OFF = 0>
 __device__ __forceinline__ void tr_issue(lds64 (&r)[4], unsigned a0, unsigned a1) {
+  static_assert(OFF + ROWB * (RB + 24) < 65536, "DS immediate offset");
   asm volatile(
       "ds_read_b64_tr_b16 %0, %4 offset:%6\n\t"
       "ds_read_b64_tr_b16 %1, %5 offset:%7\n\t"
       "ds_read_b64_tr_b16 %2, %4 offset:%8\n\t"
       "ds_read_b64_tr_b16 %3, %5 offset:%9"
       : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3])
-      : "v"(a0), "v"(a1), "i"(ROWB * RB), "i"(ROWB * (RB + 8)), "i"(ROWB * (RB + 16)), "i"(ROWB * (RB + 24)));
+      : "v"(a0), "v"(a1), "i"(OFF + ROWB * RB), "i"(OFF + ROWB * (RB + 8)), "i"(OFF + ROWB * (RB + 16)),
+        "i"(OFF + ROWB * (RB + 24)));
+}
+// LDS byte address -> pointer; a constant added to the pointer (not to the address)
+// folds into the DS instruction's immediate offset
+__device__ __forceinline__ const __attribute__((address_space(3))) char* lds_ptr(unsigned a) {
+  return reinterpret_cast<const __attribute__((address_space(3))) char*>((size_t)a);
+}
+template <class T>
+__device__ __forceinline__ T lds_at(unsigned a, int off) {
+  return *reinterpret_cast<const __attribute__((address_space(3))) T*>(lds_ptr(a) + off);
 }
 // retire every outstanding LDS read, then pin the asm results so no use of
 // them can be scheduled above the wait (cdna_hip_programming.md 5.7 item 1)
@@ -678,6 +695,9 @@ void attn_fwd_kernel(FwdParams p) {
   // static priority for the second-dispatched half (MI355X_MICROARCH.md, two waves per SIMD, item 4)
   if (NW == 8 && p.prio && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
 
+  // per-lane LDS read bases kept in registers across the loop (DTA_FWD_LBASE; see attn_dkdv_kernel)
+  int LrK = 0, LtV = 0;
+  if constexpr (sizeof(E) == 2) { LrK = row_lane<KI::ROWB>(lane); LtV = tr_lane<VI::ROWB>(lane); }
   // key = k0 + kb*32 + rowof(r); masked when key > qrow or key >= T
   auto mask_scores = [&](int k0, f32x16 (&sa)[NKB]) {
     const int lim = min(qrow, T - 1) - k0 - 4 * hf;
@@ -760,7 +780,7 @@ void attn_fwd_kernel(FwdParams p) {
       const E* Ki = Kc + i * BN * HS;
       if constexpr (sizeof(E) == 2) {
         // row operands: byte R*ROWB + (Lrow ^ 32 s) for a 32-row block at row R
-        const int Lr = row_lane<KI::ROWB>(lane);
+        const int Lr = LrK;
         const char* kbase = reinterpret_cast<const char*>(Ki);
         const char* qbase = reinterpret_cast<const char*>(Qs + (i >= NQR ? i - NQR : 0) * BM * HS) + wave * 32 * QI::ROWB;
 #pragma unroll
@@ -848,7 +868,7 @@ void attn_fwd_kernel(FwdParams p) {
     const E* Vc = Vb + (kt % NS) * BN * DVC;
     if constexpr (sizeof(E) == 2) {
       const unsigned vb = lds_addr(Vc);
-      const int Lv = tr_lane<VI::ROWB>(lane);
+      const int Lv = LtV;
       sfor<NDB>([&](auto D) {
         constexpr int d = decltype(D)::value;
         lds64 r[NKB][4];
@@ -886,6 +906,11 @@ void attn_fwd_kernel(FwdParams p) {
     // keep lane-derived addresses loop-variant: recomputed per tile instead of
     // hoisted into (spilled) registers across the whole loop
     asm volatile("" : "+v"(lane));
+    if constexpr (DTA_FWD_LBASE && sizeof(E) == 2) {
+      asm volatile("" : "+v"(LrK), "+v"(LtV));
+    } else if constexpr (sizeof(E) == 2) {
+      LrK = row_lane<KI::ROWB>(lane); LtV = tr_lane<VI::ROWB>(lane);
+    }
     tid = (wave << 6) + lane; hf = lane >> 5; c32 = lane & 31;
     qrow = qw0 + c32;
     const bool live = wave_live && kt * BN <= qw0 + 31;
@@ -1434,11 +1459,25 @@ void attn_dq_kernel(BwdParams p) {
   if (NW == 8 && p.prio && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
 
   // unmasked loop, then the block's diagonal / tail tiles (see attn_fwd_kernel)
+  // per-lane LDS read bases kept in registers across the loop (DTA_DQ_LBASE; see attn_dkdv_kernel)
+  int LrV = 0, LrK = 0, LrQ = 0, LtK = 0;
+  if constexpr (sizeof(E) == 2) {
+    LrV = row_lane<VI::ROWB>(lane); LrK = row_lane<KI::ROWB>(lane); LrQ = row_lane<QI::ROWB>(lane);
+    LtK = tr_lane<KI::ROWB>(lane);
+  }
   auto step = [&](int kt, auto MASKED) {
     constexpr bool MASK = decltype(MASKED)::value;
     // keep lane-derived addresses loop-variant: recomputed per tile instead of
     // hoisted into (spilled) registers across the whole loop
     asm volatile("" : "+v"(lane));
+    if constexpr (DTA_DQ_LBASE && sizeof(E) == 2) {
+      asm volatile("" : "+v"(LrV), "+v"(LrK), "+v"(LtK));
+      if constexpr (QI::ROWB == KI::ROWB) LrQ = LrK;
+      else asm volatile("" : "+v"(LrQ));
+    } else if constexpr (sizeof(E) == 2) {
+      LrV = row_lane<VI::ROWB>(lane); LrK = row_lane<KI::ROWB>(lane); LrQ = row_lane<QI::ROWB>(lane);
+      LtK = tr_lane<KI::ROWB>(lane);
+    }
     tid = (wave << 6) + lane; hf = lane >> 5; c32 = lane & 31;
     qrow = qw0 + c32;
     const int buf = kt % NS;
@@ -1450,7 +1489,7 @@ void attn_dq_kernel(BwdParams p) {
       {
         f32x16 dp[NKB];
         if constexpr (sizeof(E) == 2) {
-          const int Lv = row_lane<VI::ROWB>(lane);
+          const int Lv = LrV;
           const char* vbase = reinterpret_cast<const char*>(Vc);
 #pragma unroll
           for (int kb = 0; kb < NKB; ++kb) dp[kb] = f32x16{};
@@ -1474,11 +1513,11 @@ void attn_dq_kernel(BwdParams p) {
           const E* Ki = Kc + i * BN * HSP;
           f32x16 sa[NKB];
           if constexpr (sizeof(E) == 2) {
-            const int Lr = row_lane<KI::ROWB>(lane);
+            const int Lr = LrK;
             const char* kbase = reinterpret_cast<const char*>(Ki);
             const char* qbase = reinterpret_cast<const char*>(Qs + (i >= NQR ? i - NQR : 0) * BM * HS) +
                                 wave * 32 * QI::ROWB;
-            const int Lq = row_lane<QI::ROWB>(lane);
+            const int Lq = LrQ;
 #pragma unroll
             for (int kb = 0; kb < NKB; ++kb) sa[kb] = f32x16{};
             if constexpr (DTA_DQ_AHEAD && NSQ * (NKB + 1) <= 12) {
@@ -1543,7 +1582,7 @@ void attn_dq_kernel(BwdParams p) {
           // dQ_i^T += K_i^T dS_i^T
           if constexpr (sizeof(E) == 2) {
             const unsigned kbse = lds_addr(Ki);
-            const int Lk = tr_lane<KI::ROWB>(lane);
+            const int Lk = LtK;
             sfor<NHB>([&](auto D) {
               constexpr int d = decltype(D)::value;
               lds64 r[NKB][4];
@@ -1908,6 +1947,14 @@ void attn_dkdv_kernel(BwdParams p) {
   // read of a step is then one v_xad (base ^ k-step) + stage; without the switch they
   // are re-derived from the lane id each step
   int LrD = 0, LrQ = 0, LrK = 0, LtQ = 0, LtD = 0;
+  // XA: the stage base is added to each family's lane base once per step and the
+  // k-step / d-block XOR applied after it (valid: stage bases are multiples of XM, a
+  // power of two above every XOR constant); region offsets ride in DS immediates.
+  // (The dynamic LDS array starts at address 0: the kernel has no static LDS.)
+  constexpr int XMAX = 64 * ((NVB > NHB ? NVB : NHB) - 1) + 32 + 32 * ((NSV > NSQ ? NSV : NSQ) - 1);
+  constexpr int XM = XMAX < 256 ? 256 : (XMAX < 512 ? 512 : 1024);
+  constexpr bool XA = DTA_DKDV_LBASE && SRD && sizeof(E) == 2 && SUB == 1 && !STG &&
+                      (CF::nK * (int)sizeof(E)) % XM == 0 && RG::SB % XM == 0 && QI::ROWB == KI::ROWB;
   if constexpr (sizeof(E) == 2) {
     LrD = row_lane<DI::ROWB>(lane); LrQ = row_lane<QI::ROWB>(lane); LrK = row_lane<KI::ROWB>(lane);
     LtQ = tr_lane<QI::ROWB>(lane); LtD = tr_lane<DI::ROWB>(lane);
@@ -1972,6 +2019,11 @@ void attn_dkdv_kernel(BwdParams p) {
       const E* Dc = (SRD ? reinterpret_cast<const E*>(sg + RG::OFF_D) : Db + buf * BQ * DV) + so * DV;
       const float* Lc = (SRD ? reinterpret_cast<const float*>(sg + RG::OFF_L) : Lb + buf * NP) + so;
       const float* Gc = (SRD ? reinterpret_cast<const float*>(sg + RG::OFF_G) : Gb + buf * NP) + so;
+      unsigned bQ = 0, bD = 0, tQ = 0, tD = 0;
+      if constexpr (XA) {
+        const unsigned sb = lds_addr(sg);
+        bQ = LrQ + sb; bD = LrD + sb; tQ = LtQ + sb; tD = LtD + sb;
+      }
       {
       // Gc rows (attn_dq): without dropout -delta_0 | delta_0 - delta_i, and the dP
       // accumulator starts at -delta_0, so dS_0 / c_0 = P_0 dpa and dS_i / c_i =
@@ -1990,7 +2042,10 @@ void attn_dkdv_kernel(BwdParams p) {
           const int Ld = LrD;
           const char* dbase = reinterpret_cast<const char*>(Dc);
 #pragma unroll
-          for (int s = 0; s < NSV; ++s) dpa = O::mma(*reinterpret_cast<const frag*>(dbase + (Ld ^ (32 * s))), vf[s], dpa);
+          for (int s = 0; s < NSV; ++s) {
+            if constexpr (XA) dpa = O::mma(lds_at<frag>(bD ^ (32 * s), RG::OFF_D), vf[s], dpa);
+            else dpa = O::mma(*reinterpret_cast<const frag*>(dbase + (Ld ^ (32 * s))), vf[s], dpa);
+          }
         } else {
 #pragma unroll
           for (int s = 0; s < NSV; ++s) dpa = O::mma(DI::row(Dc, c32, s, hf), vf[s], dpa);
@@ -2020,7 +2075,8 @@ void attn_dkdv_kernel(BwdParams p) {
           frag qfr[NSQ], kfr[NSQ];
 #pragma unroll
           for (int s = 0; s < NSQ; ++s) {
-            qfr[s] = *reinterpret_cast<const frag*>(qbase + (Lq ^ (32 * s)));
+            if constexpr (XA) qfr[s] = lds_at<frag>(bQ ^ (32 * s), i * RG::QB);
+            else qfr[s] = *reinterpret_cast<const frag*>(qbase + (Lq ^ (32 * s)));
             kfr[s] = *reinterpret_cast<const frag*>(kbase + (Lk ^ (32 * s)));
           }
 #pragma unroll
@@ -2065,7 +2121,8 @@ void attn_dkdv_kernel(BwdParams p) {
             lds64 r[NHB][4];
             sfor<NHB>([&](auto D) {
               constexpr int d = decltype(D)::value;
-              tr_issue<QI::ROWB, 0>(r[d], qb + (Lq ^ (64 * d)), qb + (Lq ^ (64 * d + 32)));
+              if constexpr (XA) tr_issue<QI::ROWB, 0>(r[d], (tQ ^ (64 * d)) + i * RG::QB, (tQ ^ (64 * d + 32)) + i * RG::QB);
+              else tr_issue<QI::ROWB, 0>(r[d], qb + (Lq ^ (64 * d)), qb + (Lq ^ (64 * d + 32)));
             });
             lgkm_pin<NHB>(r);
             const frag p0 = O::template pack<0>(sa), p1 = O::template pack<1>(sa);
@@ -2103,7 +2160,8 @@ void attn_dkdv_kernel(BwdParams p) {
             lds64 r[NP2][4];
             sfor<NP2>([&](auto E2) {
               constexpr int d = d0 + decltype(E2)::value;
-              tr_issue<DI::ROWB, 0>(r[decltype(E2)::value], db + (Ld ^ (64 * d)), db + (Ld ^ (64 * d + 32)));
+              if constexpr (XA) tr_issue<DI::ROWB, 0, RG::OFF_D>(r[decltype(E2)::value], tD ^ (64 * d), tD ^ (64 * d + 32));
+              else tr_issue<DI::ROWB, 0>(r[decltype(E2)::value], db + (Ld ^ (64 * d)), db + (Ld ^ (64 * d + 32)));
             });
             lgkm_pin<NP2>(r);
 #pragma unroll
