@@ -153,15 +153,23 @@ class MultiHeadDiffAttention(nn.Module):
 
 
 class SwiGLU(nn.Module):
-    """silu(W_g x) * (W_x x)  (diff_transformer.py:95-105)."""
+    """silu(W_g x) * (W_x x)  (diff_transformer.py:95-105).  On the GPU the two Linears run
+    as one GEMM over shared weight / bias packs (ops.packed_swiglu)."""
 
     def __init__(self, size_in, size_out):
         super().__init__()
         self.linear_gate = nn.Linear(size_in, size_out)
         self.linear_xform = nn.Linear(size_in, size_out)
+        self._wpack = {}                           # shared storage of [W_gate; W_xform]
+        self._bpack = {}                           # ... and of [b_gate; b_xform]
+
+    def param_packs(self):
+        """(holder, params) of the shared-storage groups (dp.BucketedAllReduce)."""
+        g, x = self.linear_gate, self.linear_xform
+        return [(self._wpack, [g.weight, x.weight]), (self._bpack, [g.bias, x.bias])]
 
     def forward(self, x):
-        return ops.swiglu(self.linear_gate(x), self.linear_xform(x))
+        return ops.packed_swiglu(x, self.linear_gate, self.linear_xform, self._wpack, self._bpack)
 
 
 class Block(nn.Module):

@@ -341,6 +341,93 @@ def swiglu(a: Tensor, b: Tensor) -> Tensor:
     return _SwiGLU.apply(a, b)
 
 
+def _swiglu_launch(y2: Tensor, n: int, out: Optional[Tensor], dout: Optional[Tensor], dy: Optional[Tensor]):
+    """dta_swiglu over the column halves of a packed (rows, 2n) projection: a = y2[:, :n],
+    b = y2[:, n:]; forward writes ``out`` (rows, n), backward writes da | db into the halves
+    of ``dy`` (rows, 2n)."""
+    lib = _lib.load()
+    es, rows, w = y2.element_size(), y2.shape[0], 2 * n
+    a, b = y2.data_ptr(), y2.data_ptr() + n * es
+    if dy is None:
+        sa = _lib.SwigluArgs(_lib.dtype_code(y2.dtype), rows, n, a, w, b, w, out.data_ptr(), n,
+                             None, 0, None, 0, None, 0)
+        _lib.check(lib.dta_swiglu_fwd(sa, _lib.stream_handle(y2.device)))
+    else:
+        sa = _lib.SwigluArgs(_lib.dtype_code(y2.dtype), rows, n, a, w, b, w, None, 0, dout.data_ptr(), n,
+                             dy.data_ptr(), w, dy.data_ptr() + n * es, w)
+        _lib.check(lib.dta_swiglu_bwd(sa, _lib.stream_handle(y2.device)))
+
+
+class _PackedSwiGLU(torch.autograd.Function):
+    """SwiGLU with its gate and xform Linears as ONE GEMM over a shared weight pack
+    ``[W_gate; W_xform]`` (and bias pack): one (rows, 2n) projection whose halves feed
+    the fused SwiGLU kernel; backward writes dA | dB into one (rows, 2n) gradient, so
+    dX is one GEMM (K = 2n) instead of two plus an add, dW one GEMM and the bias
+    gradient one column sum.  Casts as autocast applies them to the two nn.Linear."""
+
+    @staticmethod
+    @torch.amp.custom_fwd(device_type="cuda")
+    def forward(ctx, x, wbase, bbase, wholder, bholder, *params):
+        dt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else x.dtype
+        xc = x.to(dt)
+        wc, bc = wbase.to(dt), bbase.view(-1).to(dt)
+        with torch.autocast("cuda", enabled=False):
+            y = F.linear(xc, wc, bc)
+        n = wc.shape[0] // 2
+        y2 = y.view(-1, 2 * n)
+        out = torch.empty(y2.shape[0], n, device=y.device, dtype=y.dtype)
+        _swiglu_launch(y2, n, out, None, None)
+        ctx.save_for_backward(xc, wc, y2)
+        ctx.x_dtype, ctx.w_dtype, ctx.n = x.dtype, wbase.dtype, n
+        ctx.wrows = [params[0].shape[0], params[1].shape[0]]
+        bound = (wholder is not None and "grad" in wholder and bholder is not None and "grad" in bholder)
+        ctx.holders = (wholder, bholder) if bound else None
+        ctx.params = params if bound else None
+        return out.view(*x.shape[:-1], n)
+
+    @staticmethod
+    @torch.amp.custom_bwd(device_type="cuda")
+    def backward(ctx, dout):
+        xc, wc, y2 = ctx.saved_tensors
+        n = ctx.n
+        d2 = dout.to(y2.dtype).contiguous().view(-1, n)
+        dy = torch.empty_like(y2)
+        _swiglu_launch(y2, n, None, d2, dy)
+        with torch.autocast("cuda", enabled=False):
+            dx = (dy @ wc).view(*xc.shape[:-1], xc.shape[-1]).to(ctx.x_dtype) if ctx.needs_input_grad[0] else None
+            dw = dy.t() @ xc.reshape(-1, xc.shape[-1])
+            db = dy.sum(0)
+        if ctx.holders is not None and all(ctx.needs_input_grad[5:]):
+            wh, bh = ctx.holders
+            gw = packing._grad_target(wh, ctx.params[:2])
+            gb = packing._grad_target(bh, ctx.params[2:])
+            if gw is not None and gb is not None:
+                gw.view_as(dw).add_(dw)             # one launch each, bf16 -> fp32 in the add
+                gb.view_as(db).add_(db)
+                for h, ps in ((wh, ctx.params[:2]), (bh, ctx.params[2:])):
+                    for p in ps:
+                        h["on_ready"](p)
+                return (dx, None, None, None, None) + (None,) * 4
+        dw = dw.to(ctx.w_dtype)
+        db = db.to(ctx.w_dtype)
+        gwg, gwx = torch.split(dw, ctx.wrows, 0)
+        gbg, gbx = torch.split(db, ctx.wrows, 0)
+        return (dx, None, None, None, None, gwg, gwx, gbg, gbx)
+
+
+def packed_swiglu(x: Tensor, gate: torch.nn.Linear, xform: torch.nn.Linear, wholder: Dict, bholder: Dict) -> Tensor:
+    """SwiGLU.forward of the reference models (silu(W_g x + b_g) * (W_x x + b_x)) with
+    both Linears' parameters as row views of shared packs (packing.ensure_packed)."""
+    wparams, bparams = [gate.weight, xform.weight], [gate.bias, xform.bias]
+    n = gate.weight.shape[0]
+    if (not x.is_cuda or n % 8 or xform.weight.shape != gate.weight.shape or gate.bias is None
+            or xform.bias is None or gate.weight.dtype != xform.weight.dtype):
+        return swiglu(gate(x), xform(x))
+    wbase = packing.ensure_packed(wparams, wholder)
+    bbase = packing.ensure_packed(bparams, bholder)
+    return _PackedSwiGLU.apply(x, wbase, bbase, wholder, bholder, *wparams, *bparams)
+
+
 # ------------------------------------------------------------------ decode ---
 def rope_rows(src: Tensor, dst: Tensor, table: Tensor) -> None:
     """dst = RoPE(src) for (B, T, H, N, hs) views whose rows are the positions of

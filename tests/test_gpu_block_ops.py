@@ -121,11 +121,47 @@ def test_swiglu_matches_torch(dtype):
 
 
 def test_swiglu_module_uses_fused_kernel():
-    """The Block's SwiGLU module routes through dta_swiglu (autograd node _SwiGLU)."""
+    """The Block's SwiGLU module routes through dta_swiglu over one packed GEMM
+    (autograd node _PackedSwiGLU)."""
     from differential_transformer_replication_amd import diff_transformer as D
     m = D.SwiGLU(64, 256).to(DEV)
     y = m(torch.randn(2, 5, 64, device=DEV))
-    assert type(y.grad_fn).__name__ == "_SwiGLUBackward"
+    assert type(y.grad_fn).__name__ == "_PackedSwiGLUBackward"
+
+
+@pytest.mark.parametrize("mode", ["fp32", "bf16"])
+def test_packed_swiglu_matches_two_linears(mode):
+    """SwiGLU with gate/xform as one packed GEMM vs the reference module's two
+    nn.Linear + silu * (diff_transformer.py:95-105), in fp64 on the CPU: output, input
+    grad and every weight / bias grad (fp32 1e-4; bf16 autocast 2e-2)."""
+    from differential_transformer_replication_amd import diff_transformer as D
+    torch.manual_seed(3)
+    m = D.SwiGLU(96, 256)
+    with torch.no_grad():
+        for p in m.parameters():
+            p.normal_(0, 0.1)
+    ref = {k: v.double().requires_grad_(True) for k, v in m.state_dict().items()}
+    x = torch.randn(3, 37, 96)
+    x64 = x.double().requires_grad_(True)
+    g = torch.randn(3, 37, 256)
+    r = F.silu(F.linear(x64, ref["linear_gate.weight"], ref["linear_gate.bias"])) * \
+        F.linear(x64, ref["linear_xform.weight"], ref["linear_xform.bias"])
+    r.backward(g.double())
+    mg = m.to(DEV)
+    xg = x.to(DEV).requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=mode == "bf16"):
+        y = mg(xg)
+    assert type(y.grad_fn).__name__ == "_PackedSwiGLUBackward"
+    y.backward(g.to(DEV).to(y.dtype))
+    tol = 1e-4 if mode == "fp32" else 2e-2
+    assert rel_err(y.float().cpu(), r) < tol
+    assert rel_err(xg.grad.float().cpu(), x64.grad) < tol
+    for n, p in mg.named_parameters():
+        assert p.grad.dtype == torch.float32
+        assert rel_err(p.grad.cpu(), ref[n].grad) < tol, n
+    # the parameters are row views of the packs; state_dict keys are the reference's
+    assert set(mg.state_dict()) == set(ref)
+    assert mg.linear_xform.weight.data_ptr() == mg.linear_gate.weight.data_ptr() + 256 * 96 * 4
 
 
 @pytest.mark.parametrize("arch", ["diff", "ndiff"])
