@@ -25,7 +25,8 @@ ABI_VERSION = 2
 EXPORTS = ("dta_attn_fwd", "dta_attn_bwd", "dta_attn_bwd_workspace_bytes", "dta_attn_bwd_dcoef_partial_bytes",
            "dta_ln_fwd", "dta_ln_bwd", "dta_ln_bwd_workspace_bytes",
            "dta_rope", "dta_cast_f32", "dta_error_string", "dta_abi_version", "dta_supported",
-           "dta_attn_decode", "dta_attn_decode_workspace_bytes", "dta_swiglu_fwd", "dta_swiglu_bwd")
+           "dta_attn_decode", "dta_attn_decode_workspace_bytes", "dta_swiglu_fwd", "dta_swiglu_bwd",
+           "dta_accumulate_f32")
 
 
 class DtaTensor(ctypes.Structure):
@@ -117,6 +118,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         lib.dta_swiglu_fwd.argtypes = [P(SwigluArgs), ctypes.c_void_p]
         lib.dta_swiglu_bwd.argtypes = [P(SwigluArgs), ctypes.c_void_p]
         lib.dta_cast_f32.argtypes = [ctypes.c_int32] * 6 + [ctypes.c_void_p, DtaTensor, ctypes.c_void_p]
+        lib.dta_accumulate_f32.argtypes = [ctypes.c_int32, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.c_void_p]
         lib.dta_attn_decode.argtypes = [P(DecodeArgs), ctypes.c_void_p]
         lib.dta_attn_decode_workspace_bytes.argtypes = [ctypes.c_int32] * 6
         lib.dta_attn_decode_workspace_bytes.restype = ctypes.c_size_t
@@ -130,7 +133,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         lib.dta_error_string.restype = ctypes.c_char_p
         lib.dta_supported.argtypes = [ctypes.c_int32] * 4
         for fn in ("dta_attn_fwd", "dta_attn_bwd", "dta_attn_decode", "dta_ln_fwd", "dta_ln_bwd", "dta_rope", "dta_cast_f32",
-                   "dta_abi_version", "dta_supported", "dta_swiglu_fwd", "dta_swiglu_bwd"):
+                   "dta_abi_version", "dta_supported", "dta_swiglu_fwd", "dta_swiglu_bwd", "dta_accumulate_f32"):
             getattr(lib, fn).restype = ctypes.c_int
         if lib.dta_abi_version() != ABI_VERSION:
             raise RuntimeError(f"libdiffattn ABI {lib.dta_abi_version()} != expected {ABI_VERSION}")

@@ -325,6 +325,13 @@ int dta_swiglu_bwd(const dta_swiglu_args* a, void* stream) {
   return status(launch_swiglu(a->dtype, p, true, (hipStream_t)stream));
 }
 
+int dta_accumulate_f32(int32_t dtype, int64_t n, const void* src, float* dst, void* stream) {
+  if (dtype < DTA_BF16 || dtype > DTA_F32 || n < 0) return DTA_ERR_INVALID;
+  if (n == 0) return DTA_OK;
+  if (!aligned_ptr(src) || !aligned_ptr(dst)) return DTA_ERR_INVALID;
+  return status(launch_accumulate(dtype, n, src, dst, (hipStream_t)stream));
+}
+
 int dta_cast_f32(int32_t dtype, int32_t B, int32_t T, int32_t H, int32_t n_terms, int32_t head_size,
                  const float* src, dta_tensor dst, void* stream) {
   if (!ok_dims(dtype, B, T, H, n_terms, head_size, 1) || head_size % 8) return DTA_ERR_INVALID;

@@ -113,5 +113,6 @@ struct SwigluParams {
   void* db; int64_t dbs;
 };
 int launch_swiglu(int dtype, const SwigluParams& p, bool bwd, hipStream_t st);
+int launch_accumulate(int dtype, int64_t n, const void* src, float* dst, hipStream_t st);
 
 }  // namespace dta

@@ -601,6 +601,36 @@ int launch_dcoef_reduce(const float* part, float* dcoef, int H, int N, int64_t p
   return (int)hipGetLastError();
 }
 
+// ---- dst += (float)src (fp32 master-gradient accumulation).  HBM-bound: 8 elements
+// per thread and step (16-byte loads of 16-bit src), grid-stride, scalar tail.
+template <class E>
+__global__ __launch_bounds__(256) void accumulate_kernel(int64_t n, const E* __restrict__ src, float* __restrict__ dst) {
+  const int64_t n8 = n / 8, stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8; i += stride) {
+    float a[8];
+    ld8<E>(src + i * 8, a);
+    f32x4 d0 = *reinterpret_cast<const f32x4*>(dst + i * 8), d1 = *reinterpret_cast<const f32x4*>(dst + i * 8 + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { d0[j] += a[j]; d1[j] += a[4 + j]; }
+    *reinterpret_cast<f32x4*>(dst + i * 8) = d0;
+    *reinterpret_cast<f32x4*>(dst + i * 8 + 4) = d1;
+  }
+  for (int64_t i = n8 * 8 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride)
+    dst[i] += (float)src[i];
+}
+
+int launch_accumulate(int dtype, int64_t n, const void* src, float* dst, hipStream_t st) {
+  const int64_t items = (n + 7) / 8;
+  const dim3 g((unsigned)std::min<int64_t>((items + 255) / 256, 256 * 16));
+  switch (dtype) {
+    case 0: hipLaunchKernelGGL(accumulate_kernel<__bf16>, g, dim3(256), 0, st, n, (const __bf16*)src, dst); break;
+    case 1: hipLaunchKernelGGL(accumulate_kernel<_Float16>, g, dim3(256), 0, st, n, (const _Float16*)src, dst); break;
+    case 2: hipLaunchKernelGGL(accumulate_kernel<float>, g, dim3(256), 0, st, n, (const float*)src, dst); break;
+    default: return -1;
+  }
+  return (int)hipGetLastError();
+}
+
 // ---- SwiGLU (diff_transformer.py / Ndiff_transformer.py / control.py SwiGLU.forward):
 // out = silu(a) * b with a = linear_gate(x), b = linear_xform(x), and its backward
 // da = dout * b * silu'(a), db = dout * silu(a), silu'(a) = s (1 + a (1 - s)), s = sigmoid(a).

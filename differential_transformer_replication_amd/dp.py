@@ -154,6 +154,18 @@ class BucketedAllReduce:
             b.handle = None
             b.pending = b.size
 
+    def clip_grad_norm_(self, max_norm: float) -> torch.Tensor:
+        """torch.nn.utils.clip_grad_norm_(params, max_norm) (train.py:273) over the flat
+        buckets the parameters' gradients are views of: the same L2 norm and scale,
+        computed with one norm and one multiply per bucket instead of one per parameter."""
+        if any(p.grad is None or id(p) not in self._owner for p in self.params):
+            return torch.nn.utils.clip_grad_norm_(self.params, max_norm)
+        flats = [b.flat for b in self.buckets]
+        total = torch.linalg.vector_norm(torch.stack(torch._foreach_norm(flats, 2.0)), 2.0)
+        coef = torch.clamp(max_norm / (total + 1e-6), max=1.0)
+        torch._foreach_mul_(flats, coef)
+        return total
+
     def zero_grad(self) -> None:
         for b in self.buckets:
             b.flat.zero_()

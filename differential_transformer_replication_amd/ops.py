@@ -402,8 +402,8 @@ class _PackedSwiGLU(torch.autograd.Function):
             gw = packing._grad_target(wh, ctx.params[:2])
             gb = packing._grad_target(bh, ctx.params[2:])
             if gw is not None and gb is not None:
-                gw.view_as(dw).add_(dw)             # one launch each, bf16 -> fp32 in the add
-                gb.view_as(db).add_(db)
+                packing.accumulate(gw, dw)          # one launch each, bf16 -> fp32 in the add
+                packing.accumulate(gb, db)
                 for h, ps in ((wh, ctx.params[:2]), (bh, ctx.params[2:])):
                     for p in ps:
                         h["on_ready"](p)

@@ -26,6 +26,7 @@ parameter to the bucket's ready hook itself, instead of autograd running one
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Sequence
 
 import torch
@@ -67,6 +68,23 @@ def bind_grad(holder: Dict, params: Sequence[torch.nn.Parameter], gflat: torch.T
     a parameter's gradient has been accumulated."""
     holder["grad"] = gflat
     holder["on_ready"] = on_ready
+
+
+_ACC_KERNEL = os.environ.get("DTA_ACC_KERNEL", "1") != "0"      # A/B switch: 0 = torch's add_
+
+
+def accumulate(g: torch.Tensor, d: torch.Tensor) -> None:
+    """g += d for an fp32 gradient buffer and a bf16/fp16/fp32 gradient of the same
+    numel: one HBM-bound HIP launch (dta_accumulate_f32) on the GPU, where torch's
+    mixed-dtype add runs at a fraction of the HBM rate."""
+    from . import _lib
+    if (_ACC_KERNEL and g.is_cuda and d.is_cuda and g.dtype == torch.float32 and d.dtype in _lib._DTYPES and g.is_contiguous()
+            and d.is_contiguous() and g.numel() == d.numel() and g.data_ptr() % 16 == 0 and d.data_ptr() % 16 == 0):
+        lib = _lib.load()
+        _lib.check(lib.dta_accumulate_f32(_lib.dtype_code(d.dtype), g.numel(), d.data_ptr(), g.data_ptr(),
+                                          _lib.stream_handle(g.device)))
+    else:
+        g.view_as(d).add_(d)
 
 
 def _grad_target(holder: Dict, params: Sequence[torch.nn.Parameter]):
@@ -111,7 +129,7 @@ class _PackedLinear(torch.autograd.Function):
         if ctx.holder is not None and all(ctx.needs_input_grad[3:]):
             g = _grad_target(ctx.holder, ctx.params)
             if g is not None:
-                g.view_as(dw).add_(dw)            # one launch, bf16 -> fp32 in the add
+                accumulate(g, dw)                 # one launch, bf16 -> fp32 in the add
                 hook = ctx.holder["on_ready"]
                 for p in ctx.params:
                     hook(p)
@@ -140,7 +158,7 @@ class _PackedParams(torch.autograd.Function):
         if ctx.holder is not None and all(ctx.needs_input_grad[2:]):
             g = _grad_target(ctx.holder, ctx.params)
             if g is not None:
-                g.view_as(d).add_(d)
+                accumulate(g, d)
                 hook = ctx.holder["on_ready"]
                 for p in ctx.params:
                     hook(p)

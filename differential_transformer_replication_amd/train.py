@@ -195,6 +195,9 @@ def setup_distributed(cfg: TrainingConfig):
     return world, rank, dev
 
 
+_BUCKET_CLIP = os.environ.get("DTA_BUCKET_CLIP", "1") != "0"    # A/B switch: 0 = per-parameter clip
+
+
 class Trainer:
     """One optimizer step = grad_acc_steps micro-steps + DP sync + clip + AdamW."""
 
@@ -225,7 +228,10 @@ class Trainer:
         self.sync.synchronize()
         if self.scaler is not None:
             self.scaler.unscale_(self.opt)
-        torch.nn.utils.clip_grad_norm_(self.model.parameters(), 1.0)
+        if _BUCKET_CLIP:                 # clip_grad_norm_(model.parameters(), 1.0) over the buckets
+            self.sync.clip_grad_norm_(1.0)
+        else:
+            torch.nn.utils.clip_grad_norm_(self.model.parameters(), 1.0)
         if self.scaler is not None:
             self.scaler.step(self.opt)
             self.scaler.update()

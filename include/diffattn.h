@@ -234,6 +234,12 @@ typedef struct {
 int dta_swiglu_fwd(const dta_swiglu_args* a, void* stream);
 int dta_swiglu_bwd(const dta_swiglu_args* a, void* stream);
 
+/* dst[i] += (float)src[i], i < n: gradient accumulation of a bf16/fp16/fp32 weight
+ * gradient into fp32 master-gradient storage (the training step's packed projection
+ * weights, SURVEY 8e/8f: torch.autograd's AccumulateGrad of the reference's
+ * nn.Linear parameters, train.py:251-279).  src and dst 16-byte aligned. */
+int dta_accumulate_f32(int32_t dtype, int64_t n, const void* src, float* dst, void* stream);
+
 /* Cast/copy a [b][t][h][i][d] tensor from fp32 to dtype (dQ finalisation). */
 int dta_cast_f32(int32_t dtype, int32_t B, int32_t T, int32_t H, int32_t n_terms,
                  int32_t head_size, const float* src, dta_tensor dst, void* stream);

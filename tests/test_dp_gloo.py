@@ -178,3 +178,26 @@ def test_bench_cpu_dry_run_two_ranks():
     bad = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--device", "cpu"],
                          capture_output=True, text=True, timeout=120, env=dict(env, WORLD_SIZE="1"))
     assert bad.returncode == 2                # --gpus disagrees with the launcher's WORLD_SIZE
+
+
+@pytest.mark.parametrize("scale", [0.01, 100.0])
+def test_bucket_clip_matches_torch_clip(scale):
+    """BucketedAllReduce.clip_grad_norm_ (one norm / multiply per bucket) gives the
+    norm and the clipped gradients of torch.nn.utils.clip_grad_norm_ (train.py:273),
+    below and above the max norm, over several buckets."""
+    torch.manual_seed(0)
+    ref, m = Net(), Net()
+    m.load_state_dict(ref.state_dict())
+    sync = BucketedAllReduce(m, bucket_cap_mb=0.002)
+    assert len(sync.buckets) > 1
+    x = torch.randn(8, 16)
+    (ref(x).sum() * scale).backward()
+    (m(x).sum() * scale).backward()
+    for p in ref.parameters():
+        if p.grad is None:
+            p.grad = torch.zeros_like(p)
+    n_ref = torch.nn.utils.clip_grad_norm_(ref.parameters(), 1.0)
+    n = sync.clip_grad_norm_(1.0)
+    assert torch.allclose(n, n_ref, rtol=1e-6)
+    for (k, a), (_, b) in zip(ref.named_parameters(), m.named_parameters()):
+        assert torch.allclose(a.grad, b.grad, rtol=1e-6, atol=1e-9), k

@@ -194,3 +194,18 @@ def test_bound_gradients_equal_autograd(arch):
     torch.cuda.synchronize()
     for (n, a), (_, b) in zip(ref.named_parameters(), m.named_parameters()):
         assert torch.equal(a.grad, b.grad), n
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("n", [8, 1000, 1 << 20, (1 << 20) + 5])
+def test_accumulate_f32(dtype, n):
+    """dta_accumulate_f32 (packing.accumulate): fp32 g += d for the packed-gradient
+    buckets, bitwise equal to torch's fp32 add of the upcast gradient (tail included)."""
+    from differential_transformer_replication_amd import packing
+    gen = torch.Generator().manual_seed(n)
+    g = torch.randn(n, generator=gen).to(DEV)
+    d = torch.randn(n, generator=gen).to(dtype).to(DEV)
+    ref = g + d.float()
+    packing.accumulate(g, d)
+    torch.cuda.synchronize()
+    assert torch.equal(g, ref)
