@@ -72,8 +72,14 @@
 #ifndef DTA_DKDV_SPLIT
 #define DTA_DKDV_SPLIT 0
 #endif
+#ifndef DTA_FWD_PREOFF   // forward: per-lane K/V DMA source offsets in VGPRs, computed once
+#define DTA_FWD_PREOFF 1
+#endif
+#ifndef DTA_DQ_PREOFF    // dQ: the same
+#define DTA_DQ_PREOFF 1
+#endif
 #ifndef DTA_DKDV_PREOFF
-#define DTA_DKDV_PREOFF 0
+#define DTA_DKDV_PREOFF 1
 #endif
 // forward: the two waves of a SIMD run half a tile apart (see attn_fwd_kernel)
 #ifndef DTA_FWD_PINGPONG
@@ -632,9 +638,15 @@ void attn_fwd_kernel(FwdParams p) {
   const int kend = min(T, q0 + BM);
   const int ntiles = (kend + BN - 1) / BN;
   using KR = KvRing<E, HS, N, DVC, BN, NW>;
+  // DTA_FWD_PREOFF: this wave's per-lane DMA source offsets computed once (VGPRs)
+  constexpr bool PRE = DTA_FWD_PREOFF && SRD;
+  uint32_t doff[PRE ? KR::MYP : 1];
+  if constexpr (PRE) KR::offsets(p.k.st, p.k.si, p.v.st, wave, lane, doff);
   auto stage_kv = [&](int kt, int buf) {
     const int k0 = kt * BN;
-    if constexpr (SRD) {
+    if constexpr (PRE) {
+      KR::issue_pre(gk, p.k.st, gv, p.v.st, k0, T, Kb + buf * N * BN * HS, Vb + buf * BN * DVC, wave, doff);
+    } else if constexpr (SRD) {
       KR::issue(gk, p.k.st, p.k.si, gv, p.v.st, k0, T, Kb + buf * N * BN * HS, Vb + buf * BN * DVC, wave, lane);
     } else {
 #pragma unroll
@@ -1375,9 +1387,14 @@ void attn_dq_kernel(BwdParams p) {
   const int ntiles = (kend + BN - 1) / BN;
   using KR = KvRing<E, HS, N, DV, BN, NW>;
   static_assert(!SRD || HSP == HS, "descriptor staging needs unpadded K rows");
+  constexpr bool PRE = DTA_DQ_PREOFF && SRD;     // per-lane DMA source offsets computed once
+  uint32_t doff[PRE ? KR::MYP : 1];
+  if constexpr (PRE) KR::offsets(p.k.st, p.k.si, p.v.st, wave, lane, doff);
   auto stage_kv = [&](int kt, int buf) {
     const int k0 = kt * BN;
-    if constexpr (SRD) {
+    if constexpr (PRE) {
+      KR::issue_pre(gk, p.k.st, gv, p.v.st, k0, T, Kb + buf * N * BN * HSP, Vb + buf * BN * DV, wave, doff);
+    } else if constexpr (SRD) {
       KR::issue(gk, p.k.st, p.k.si, gv, p.v.st, k0, T, Kb + buf * N * BN * HSP, Vb + buf * BN * DV, wave, lane);
     } else {
 #pragma unroll
