@@ -52,7 +52,7 @@
 #define DTA_FWD_LBASE 1
 #endif
 #ifndef DTA_DQ_LBASE     // dQ: per-lane LDS read bases kept in registers across the loop
-#define DTA_DQ_LBASE 0   // measured +2% on dQ at cfg2 (253 VGPRs): off
+#define DTA_DQ_LBASE 1   // with the DMA offsets precomputed and XA addressing: dQ 1.020 -> 0.994 ms
 #endif
 #ifndef DTA_DKDV_LBASE   // dK/dV: per-lane LDS read bases kept in registers across the loop
 #define DTA_DKDV_LBASE 1
@@ -1478,6 +1478,11 @@ void attn_dq_kernel(BwdParams p) {
   // unmasked loop, then the block's diagonal / tail tiles (see attn_fwd_kernel)
   // per-lane LDS read bases kept in registers across the loop (DTA_DQ_LBASE; see attn_dkdv_kernel)
   int LrV = 0, LrK = 0, LrQ = 0, LtK = 0;
+  // XA (see attn_dkdv_kernel): the ring slot's base added once per step, the k-step XOR after it
+  constexpr int XMAX = 32 * ((NSV > NSQ ? NSV : NSQ) - 1) + 64 * (NHB - 1) + 32;
+  constexpr int XM = XMAX < 256 ? 256 : (XMAX < 512 ? 512 : 1024);
+  constexpr bool XA = DTA_DQ_LBASE && SRD && sizeof(E) == 2 && (CF::nQ * (int)sizeof(E)) % XM == 0 &&
+                      (CF::nK * (int)sizeof(E)) % XM == 0 && (CF::nV * (int)sizeof(E)) % XM == 0;
   if constexpr (sizeof(E) == 2) {
     LrV = row_lane<VI::ROWB>(lane); LrK = row_lane<KI::ROWB>(lane); LrQ = row_lane<QI::ROWB>(lane);
     LtK = tr_lane<KI::ROWB>(lane);
@@ -1503,6 +1508,10 @@ void attn_dq_kernel(BwdParams p) {
     if (wave_live && k0 <= qw0 + 31) {
       const E* Kc = Kb + buf * N * BN * HSP;
       const E* Vc = Vb + buf * BN * DV;
+      unsigned bV = 0, bK = 0, tK = 0;
+      if constexpr (XA) {
+        bV = LrV + lds_addr(Vc); bK = LrK + lds_addr(Kc); tK = LtK + lds_addr(Kc);
+      }
       {
         f32x16 dp[NKB];
         if constexpr (sizeof(E) == 2) {
@@ -1514,8 +1523,10 @@ void attn_dq_kernel(BwdParams p) {
           for (int s = 0; s < NSV; ++s) {
             const int o = Lv ^ (32 * s);
 #pragma unroll
-            for (int kb = 0; kb < NKB; ++kb)
-              dp[kb] = O::mma(*reinterpret_cast<const frag*>(vbase + kb * 32 * VI::ROWB + o), df[s], dp[kb]);
+            for (int kb = 0; kb < NKB; ++kb) {
+              if constexpr (XA) dp[kb] = O::mma(lds_at<frag>(bV ^ (32 * s), kb * 32 * VI::ROWB), df[s], dp[kb]);
+              else dp[kb] = O::mma(*reinterpret_cast<const frag*>(vbase + kb * 32 * VI::ROWB + o), df[s], dp[kb]);
+            }
           }
         } else {
 #pragma unroll
@@ -1562,8 +1573,13 @@ void attn_dq_kernel(BwdParams p) {
               if (i < NQR) qb = qf[i < NQR ? i : 0][s];
               else qb = *reinterpret_cast<const frag*>(qbase + (Lq ^ (32 * s)));
 #pragma unroll
-              for (int kb = 0; kb < NKB; ++kb)
-                sa[kb] = O::mma(*reinterpret_cast<const frag*>(kbase + kb * 32 * KI::ROWB + (Lr ^ (32 * s))), qb, sa[kb]);
+              for (int kb = 0; kb < NKB; ++kb) {
+                if constexpr (XA)
+                  sa[kb] = O::mma(lds_at<frag>(bK ^ (32 * s), (i * BN * HSP) * (int)sizeof(E) + kb * 32 * KI::ROWB), qb,
+                                  sa[kb]);
+                else
+                  sa[kb] = O::mma(*reinterpret_cast<const frag*>(kbase + kb * 32 * KI::ROWB + (Lr ^ (32 * s))), qb, sa[kb]);
+              }
             }
             }
           } else {
@@ -1603,7 +1619,9 @@ void attn_dq_kernel(BwdParams p) {
             sfor<NHB>([&](auto D) {
               constexpr int d = decltype(D)::value;
               lds64 r[NKB][4];
-              const unsigned a0 = kbse + (Lk ^ (64 * d)), a1 = kbse + (Lk ^ (64 * d + 32));
+              const unsigned a0 = XA ? (tK ^ (64 * d)) + (unsigned)(i * BN * HSP * (int)sizeof(E)) : kbse + (Lk ^ (64 * d));
+              const unsigned a1 = XA ? (tK ^ (64 * d + 32)) + (unsigned)(i * BN * HSP * (int)sizeof(E))
+                                     : kbse + (Lk ^ (64 * d + 32));
               sfor<NKB>([&](auto KB) { tr_issue<KI::ROWB, 32 * decltype(KB)::value>(r[decltype(KB)::value], a0, a1); });
               lgkm_pin<NKB>(r);
 #pragma unroll
