@@ -163,7 +163,7 @@ class MultiHeadAlternatingDiffAttention(nn.Module):
                                  dropout_p=attn_dropout_p([h.dropout for h in self.heads], self.training))
         gn = self.group_norm
         out = ops.group_ln_scale(out, gn.weight, gn.bias, gn.eps, mha_out_scale(self.lambda_init), gn._gpack)
-        return self.dropout(self.proj(out))
+        return self.dropout(ops.linear(out, self.proj))
 
 
 class Block(nn.Module):
@@ -179,7 +179,7 @@ class Block(nn.Module):
 
     def forward(self, x, layer_idx):
         x = x + self.diff_attn(self.ln1(x), layer_idx)
-        return x + self.ffwd(self.ln2(x))
+        return x + ops.ffn(self.ffwd, self.ln2(x))
 
 
 class AlternatingDiffTransformer(nn.Module):

@@ -109,7 +109,7 @@ class MultiHeadAttention(nn.Module):
             q, k = _rope_fp32(q, fc), _rope_fp32(k, fc)
             out = F.scaled_dot_product_attention(q, k, v, is_causal=True, dropout_p=p, scale=1.0 / (hs ** 0.5))
             out = out.transpose(1, 2).reshape(B, T, H * hs)
-        return self.dropout(self.proj(out))
+        return self.dropout(ops.linear(out, self.proj))
 
 
 class SwiGLU(nn.Module):
@@ -144,7 +144,7 @@ class Block(nn.Module):
 
     def forward(self, x):
         x = x + self.attn(self.ln1(x))
-        return x + self.ffwd(self.ln2(x))
+        return x + ops.ffn(self.ffwd, self.ln2(x))
 
 
 class StandardTransformer(nn.Module):

@@ -149,7 +149,7 @@ class MultiHeadDiffAttention(nn.Module):
         # GroupLayerNorm then x(1 - lambda_init) with the MHA's own, never-updated 0.8 buffer
         gn = self.group_norm
         out = ops.group_ln_scale(out, gn.weight, gn.bias, gn.eps, mha_out_scale(self.lambda_init), gn._gpack)
-        return self.dropout(self.proj(out))
+        return self.dropout(ops.linear(out, self.proj))
 
 
 class SwiGLU(nn.Module):
@@ -185,7 +185,7 @@ class Block(nn.Module):
 
     def forward(self, x, layer_idx):
         x = x + self.diff_attn(self.ln1(x), layer_idx)
-        return x + self.ffwd(self.ln2(x))
+        return x + ops.ffn(self.ffwd, self.ln2(x))
 
 
 class DiffTransformer(nn.Module):

@@ -395,7 +395,7 @@ class _PackedSwiGLU(torch.autograd.Function):
         _swiglu_launch(y2, n, None, d2, dy)
         with torch.autocast("cuda", enabled=False):
             dx = (dy @ wc).view(*xc.shape[:-1], xc.shape[-1]).to(ctx.x_dtype) if ctx.needs_input_grad[0] else None
-            dw = dy.t() @ xc.reshape(-1, xc.shape[-1])
+            dw = packing.weight_grad(dy, xc.reshape(-1, xc.shape[-1]))
             db = dy.sum(0)
         if ctx.holders is not None and all(ctx.needs_input_grad[5:]):
             wh, bh = ctx.holders
@@ -413,6 +413,49 @@ class _PackedSwiGLU(torch.autograd.Function):
         gwg, gwx = torch.split(dw, ctx.wrows, 0)
         gbg, gbx = torch.split(db, ctx.wrows, 0)
         return (dx, None, None, None, None, gwg, gwx, gbg, gbx)
+
+
+class _Linear(torch.autograd.Function):
+    """``nn.Linear`` under the same autocast casts, with its weight gradient through
+    ``packing.weight_grad`` (fp32 output, split over tokens when the output is small)."""
+
+    @staticmethod
+    @torch.amp.custom_fwd(device_type="cuda")
+    def forward(ctx, x, w, b):
+        dt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else x.dtype
+        xc, wc = x.to(dt), w.to(dt)
+        bc = b.to(dt) if b is not None else None
+        with torch.autocast("cuda", enabled=False):
+            y = F.linear(xc, wc, bc)
+        ctx.save_for_backward(xc, wc)
+        ctx.dtypes = (x.dtype, w.dtype, b.dtype if b is not None else None)
+        return y
+
+    @staticmethod
+    @torch.amp.custom_bwd(device_type="cuda")
+    def backward(ctx, dy):
+        xc, wc = ctx.saved_tensors
+        xdt, wdt, bdt = ctx.dtypes
+        dy2 = dy.to(wc.dtype).reshape(-1, wc.shape[0])
+        with torch.autocast("cuda", enabled=False):
+            dx = (dy2 @ wc).view(*xc.shape[:-1], wc.shape[1]).to(xdt) if ctx.needs_input_grad[0] else None
+            dw = packing.weight_grad(dy2, xc.reshape(-1, xc.shape[-1])).to(wdt) if ctx.needs_input_grad[1] else None
+            db = dy2.sum(0).to(bdt) if bdt is not None and ctx.needs_input_grad[2] else None
+        return dx, dw, db
+
+
+def linear(x: Tensor, mod: torch.nn.Linear) -> Tensor:
+    """``mod(x)`` for the reference's nn.Linear layers on the hot path's callers (the MHA
+    output projection, the FFN output); GPU: ``_Linear``, else the module itself."""
+    if not x.is_cuda or not x.is_floating_point():
+        return mod(x)
+    return _Linear.apply(x, mod.weight, mod.bias)
+
+
+def ffn(seq: torch.nn.Sequential, x: Tensor) -> Tensor:
+    """The Block's ``ffwd = Sequential(SwiGLU, Linear(4C, C), Dropout)`` (diff_transformer.py:114-119)
+    with its Linear through ``linear``."""
+    return seq[2](linear(seq[0](x), seq[1]))
 
 
 def packed_swiglu(x: Tensor, gate: torch.nn.Linear, xform: torch.nn.Linear, wholder: Dict, bholder: Dict) -> Tensor:

@@ -71,6 +71,29 @@ def bind_grad(holder: Dict, params: Sequence[torch.nn.Parameter], gflat: torch.T
 
 
 _ACC_KERNEL = os.environ.get("DTA_ACC_KERNEL", "1") != "0"      # A/B switch: 0 = torch's add_
+_SPLITK = os.environ.get("DTA_SPLITK", "1") != "0"              # A/B switch: 0 = one bf16-output GEMM
+
+
+def weight_grad(dy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+    """dW = dy^T x for token-major (K, O) / (K, I) operands, the weight gradient of a
+    Linear over K tokens.  bf16 on the GPU: fp32 output (no bf16 rounding of dW) and,
+    when the (O, I) output has few 256x256 tiles for 256 CUs, split over K into S
+    batched GEMMs of K/S tokens whose fp32 partials are summed (measured at the cfg4
+    shapes, tools/gemm_splitk_probe.py: 1024x1024 199 -> 82 us, 3072x1024 304 -> 207,
+    8192x1024 648 -> 590).  Otherwise the plain GEMM in the operands' dtype."""
+    K, O = dy.shape
+    I = x.shape[1]
+    if not (_SPLITK and dy.is_cuda and dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16):
+        return dy.t() @ x
+    tiles = -(-O // 256) * -(-I // 256)
+    S = 8 if tiles <= 16 else (4 if tiles <= 128 else 1)
+    while S > 1 and (K % S or (K // S) % 256):
+        S //= 2
+    if S == 1:
+        return torch.mm(dy.t(), x, out_dtype=torch.float32)
+    Kc = K // S
+    part = torch.bmm(dy.view(S, Kc, O).transpose(1, 2), x.view(S, Kc, I), out_dtype=torch.float32)
+    return part.sum(0)
 
 
 def accumulate(g: torch.Tensor, d: torch.Tensor) -> None:
@@ -125,7 +148,7 @@ class _PackedLinear(torch.autograd.Function):
         dy = dy.to(wc.dtype)
         with torch.autocast("cuda", enabled=False):
             dx = (dy @ wc).to(ctx.x_dtype) if ctx.needs_input_grad[0] else None
-            dw = dy.reshape(-1, dy.shape[-1]).t() @ xc.reshape(-1, xc.shape[-1])
+            dw = weight_grad(dy.reshape(-1, dy.shape[-1]), xc.reshape(-1, xc.shape[-1]))
         if ctx.holder is not None and all(ctx.needs_input_grad[3:]):
             g = _grad_target(ctx.holder, ctx.params)
             if g is not None:

@@ -209,3 +209,44 @@ def test_accumulate_f32(dtype, n):
     packing.accumulate(g, d)
     torch.cuda.synchronize()
     assert torch.equal(g, ref)
+
+
+@pytest.mark.parametrize("O,I", [(1024, 1024), (3072, 1024), (512, 256), (96, 40)])
+def test_weight_grad_split_k(O, I):
+    """packing.weight_grad (dW = dy^T x, fp32 output, split over tokens for small
+    outputs) against an fp64 product of the same bf16 operands."""
+    from differential_transformer_replication_amd import packing
+    K = 4096
+    gen = torch.Generator().manual_seed(O + I)
+    dy = torch.randn(K, O, generator=gen).to(torch.bfloat16)
+    x = torch.randn(K, I, generator=gen).to(torch.bfloat16)
+    ref = dy.double().t() @ x.double()
+    dw = packing.weight_grad(dy.to(DEV), x.to(DEV))
+    assert dw.dtype == torch.float32 and dw.shape == (O, I)
+    assert rel_err(dw.cpu(), ref) < 1e-5
+
+
+@pytest.mark.parametrize("mode", ["fp32", "bf16"])
+def test_linear_op_matches_nn_linear(mode):
+    """ops.linear (the MHA output projection and FFN output Linear) vs nn.Linear in fp64:
+    output, input grad, weight and bias grads (fp32 1e-4; bf16 autocast 2e-2)."""
+    from differential_transformer_replication_amd import ops as O_
+    torch.manual_seed(4)
+    lin = torch.nn.Linear(256, 128)
+    ref = torch.nn.Linear(256, 128).double()
+    ref.load_state_dict({k: v.double() for k, v in lin.state_dict().items()})
+    x = torch.randn(2, 300, 256)
+    x64 = x.double().requires_grad_(True)
+    g = torch.randn(2, 300, 128)
+    ref(x64).backward(g.double())
+    lg = lin.to(DEV)
+    xg = x.to(DEV).requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=mode == "bf16"):
+        y = O_.linear(xg, lg)
+    y.backward(g.to(DEV).to(y.dtype))
+    tol = 1e-4 if mode == "fp32" else 2e-2
+    assert rel_err(y.float().cpu(), ref(x64).detach()) < tol
+    assert rel_err(xg.grad.float().cpu(), x64.grad) < tol
+    assert lg.weight.grad.dtype == torch.float32
+    assert rel_err(lg.weight.grad.cpu(), ref.weight.grad) < tol
+    assert rel_err(lg.bias.grad.cpu(), ref.bias.grad) < tol
