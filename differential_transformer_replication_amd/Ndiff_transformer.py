@@ -178,8 +178,9 @@ class Block(nn.Module):
         self.ln2 = ops.LayerNorm(n_embd, autocast_out=True)
 
     def forward(self, x, layer_idx):
-        x = x + self.diff_attn(self.ln1(x), layer_idx)
-        return x + ops.ffn(self.ffwd, self.ln2(x))
+        # the residual add and ln2 in one pass on the GPU (ops.add_layer_norm)
+        x, h = ops.add_layer_norm(x, self.diff_attn(self.ln1(x), layer_idx), self.ln2)
+        return x + ops.ffn(self.ffwd, h)
 
 
 class AlternatingDiffTransformer(nn.Module):

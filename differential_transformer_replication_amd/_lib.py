@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get("DTA_LIB", os.path.join(_HERE, "lib", "libdiffattn.so"
 DTA_BF16, DTA_F16, DTA_F32 = 0, 1, 2
 _DTYPES = {torch.bfloat16: DTA_BF16, torch.float16: DTA_F16, torch.float32: DTA_F32}
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 # every symbol include/diffattn.h declares
 EXPORTS = ("dta_attn_fwd", "dta_attn_bwd", "dta_attn_bwd_workspace_bytes", "dta_attn_bwd_dcoef_partial_bytes",
@@ -77,7 +77,10 @@ class LnArgs(ctypes.Structure):
                 ("mean", ctypes.c_void_p), ("rstd", ctypes.c_void_p),
                 ("dy", ctypes.c_void_p), ("dy_stride", ctypes.c_int64),
                 ("dx", ctypes.c_void_p), ("dx_stride", ctypes.c_int64),
-                ("dw", ctypes.c_void_p), ("db", ctypes.c_void_p), ("partial", ctypes.c_void_p), ("io_dtype", ctypes.c_int32)]
+                ("dw", ctypes.c_void_p), ("db", ctypes.c_void_p), ("partial", ctypes.c_void_p), ("io_dtype", ctypes.c_int32),
+                ("res", ctypes.c_void_p), ("res_stride", ctypes.c_int64), ("xo", ctypes.c_void_p),
+                ("xo_stride", ctypes.c_int64), ("dres", ctypes.c_void_p), ("dres_stride", ctypes.c_int64),
+                ("dx16", ctypes.c_void_p), ("dx16_stride", ctypes.c_int64)]
 
 
 class RopeArgs(ctypes.Structure):

@@ -143,8 +143,9 @@ class Block(nn.Module):
         self.ln2 = ops.LayerNorm(n_embd, autocast_out=True)
 
     def forward(self, x):
-        x = x + self.attn(self.ln1(x))
-        return x + ops.ffn(self.ffwd, self.ln2(x))
+        # the residual add and ln2 in one pass on the GPU (ops.add_layer_norm)
+        x, h = ops.add_layer_norm(x, self.attn(self.ln1(x)), self.ln2)
+        return x + ops.ffn(self.ffwd, h)
 
 
 class StandardTransformer(nn.Module):

@@ -260,6 +260,13 @@ static int ln_common(const dta_ln_args* a, bool bwd) {
   if (!bwd && (!aligned_ptr(a->y) || a->y_stride % v || !a->b)) return DTA_ERR_INVALID;
   if (bwd && (!aligned_ptr(a->dy) || !aligned_ptr(a->dx) || a->dy_stride % v || a->dx_stride % v || !a->dw || !a->db))
     return DTA_ERR_INVALID;
+  // residual fusion: the mixed fp32 / 16-bit path only, with aligned 8-element rows
+  const bool fused = bwd ? (a->dres || a->dx16) : (a->res || a->xo);
+  if (fused && a->io_dtype == 0) return DTA_ERR_UNSUPPORTED;
+  if (!bwd && fused && (!aligned_ptr(a->res) || !aligned_ptr(a->xo) || a->res_stride % v || a->xo_stride % v))
+    return DTA_ERR_INVALID;
+  if (bwd && a->dres && (!aligned_ptr(a->dres) || a->dres_stride % v)) return DTA_ERR_INVALID;
+  if (bwd && a->dx16 && (!aligned_ptr(a->dx16) || a->dx16_stride % v)) return DTA_ERR_INVALID;
   return DTA_OK;
 }
 
@@ -271,6 +278,8 @@ static LnParams ln_params(const dta_ln_args* a) {
   p.dy = a->dy; p.dys = a->dy_stride; p.dx = a->dx; p.dxs = a->dx_stride;
   p.dw = a->dw; p.db = a->db;
   p.partial = a->partial;
+  p.res = a->res; p.ress = a->res_stride; p.xo = a->xo; p.xos = a->xo_stride;
+  p.dres = a->dres; p.dress = a->dres_stride; p.dx16 = a->dx16; p.dx16s = a->dx16_stride;
   return p;
 }
 

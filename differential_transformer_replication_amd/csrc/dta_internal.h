@@ -63,6 +63,11 @@ struct LnParams {
   void* dx; int64_t dxs;
   float* dw; float* db;
   float* partial;      // optional [blocks][2][C] workspace: deterministic dw/db (no atomics)
+  // residual fusion (mixed fp32 x / 16-bit y path only; NULL = off):
+  const void* res; int64_t ress;   // fwd: x + res (res in y's dtype) is normalised ...
+  float* xo; int64_t xos;          // ... and written here (fp32)
+  const float* dres; int64_t dress;  // bwd: dx += dres (the residual branch's gradient)
+  void* dx16; int64_t dx16s;       // bwd: dx also stored in y's dtype
 };
 int launch_ln_mixed(int y_dtype, const LnParams& p, bool bwd, hipStream_t st);   // x fp32, y / dy 16-bit
 int ln_bwd_blocks(int64_t rows);

@@ -62,11 +62,23 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(LnParams p) {
   const E* x = reinterpret_cast<const E*>(p.x) + row * p.xs;
   float v[CH][8];
   float s = 0.f;
+  // residual fusion (fp32 x, 16-bit y): v = x + res, stored to xo, then normalised
+  constexpr bool MIXED = std::is_same<E, float>::value && sizeof(Y) == 2;
+  const bool fuse = MIXED && p.res != nullptr;
 #pragma unroll
   for (int c = 0; c < CH; ++c) {
     const int col = (c * 64 + lane) * 8;
     if (col < p.C) {
       ld8<E>(x + col, v[c]);
+      if constexpr (MIXED) {
+        if (fuse) {
+          float r[8];
+          ld8<Y>(reinterpret_cast<const Y*>(p.res) + row * p.ress + col, r);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[c][j] += r[j];
+          st8<float>(p.xo + row * p.xos + col, v[c]);
+        }
+      }
 #pragma unroll
       for (int j = 0; j < 8; ++j) s += v[c][j];
     }
@@ -313,6 +325,15 @@ __global__ __launch_bounds__(256) void ln_bwd_rb_kernel(LnParams p) {
         float o[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = rstd * (g[c][j] - mg - xh[c][j] * mgx);
+        if constexpr (std::is_same<E, float>::value && Y16) {
+          if (p.dres) {                        // residual fusion: + the residual branch's gradient
+            float d[8];
+            ld8<float>(p.dres + r * p.dress + col, d);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o[j] += d[j];
+          }
+          if (p.dx16) st8<Y>(reinterpret_cast<Y*>(p.dx16) + r * p.dx16s + col, o);
+        }
         st8<E>(dx + col, o);
       }
     }

@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import contextlib
 import math
+import os
 from typing import Dict, List, Optional, Tuple
 
 import torch
@@ -259,6 +260,92 @@ class _GroupLNScale(torch.autograd.Function):
                 hook(p)
             return dx.view(xshape), None, None, None, None, None, None
         return dx.view(xshape), dw.to(wdt).view(wshape), db.to(bdt).view(bshape), None, None, None, None
+
+
+class _AddLN(torch.autograd.Function):
+    """(x + a, LayerNorm(x + a)) in one pass: a Block's residual add feeding its next
+    pre-LN (diff_transformer.py:121-125), fp32 residual stream x, 16-bit branch output a
+    and LN output.  Backward: the residual gradient d(x + a) plus the LN backward, in one
+    pass that also writes the branch's 16-bit gradient."""
+
+    @staticmethod
+    def forward(ctx, x: Tensor, a: Tensor, w: Tensor, b: Tensor, eps: float, holder, ydt: torch.dtype):
+        lib = _lib.load()
+        _require_gpu(x, a, w, b)
+        C = x.shape[-1]
+        x2 = x.contiguous().view(-1, C)
+        a2 = a.to(ydt).contiguous().view(-1, C)
+        rows = x2.shape[0]
+        w32 = w.detach().to(torch.float32).contiguous().view(-1)
+        b32 = b.detach().to(torch.float32).contiguous().view(-1)
+        xo = torch.empty_like(x2)
+        y = torch.empty(x2.shape, device=x.device, dtype=ydt)
+        mean = torch.empty(rows, device=x.device, dtype=torch.float32)
+        rstd = torch.empty_like(mean)
+        io = 1 + _lib.dtype_code(ydt)
+        args = _lib.LnArgs(_lib.DTA_F32, rows, C, eps, 1.0, x2.data_ptr(), C, y.data_ptr(), C,
+                           w32.data_ptr(), b32.data_ptr(), mean.data_ptr(), rstd.data_ptr(), None, 0, None, 0,
+                           None, None, None, io, a2.data_ptr(), C, xo.data_ptr(), C)
+        _lib.check(lib.dta_ln_fwd(args, _lib.stream_handle(x.device)))
+        ctx.bound = (holder, (w, b)) if holder is not None and "grad" in holder else None
+        ctx.save_for_backward(xo, w32, mean, rstd)
+        ctx.meta = (eps, x.shape, a.dtype, ydt, w.dtype, w.shape, b.dtype, b.shape, io)
+        return xo.view(x.shape), y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dxo: Optional[Tensor], dy: Optional[Tensor]):
+        lib = _lib.load()
+        xo, w32, mean, rstd = ctx.saved_tensors
+        eps, xshape, adt, ydt, wdt, wshape, bdt, bshape, io = ctx.meta
+        C = xo.shape[1]
+        dy2 = (dy.to(ydt).contiguous().view(-1, C) if dy is not None
+               else torch.zeros(xo.shape, device=xo.device, dtype=ydt))
+        dres = dxo.to(torch.float32).contiguous().view(-1, C) if dxo is not None else None
+        dx = torch.empty_like(xo)
+        da = torch.empty(xo.shape, device=xo.device, dtype=ydt)
+        g = None
+        if ctx.bound is not None and ctx.needs_input_grad[2] and ctx.needs_input_grad[3]:
+            holder, params = ctx.bound
+            g = packing._grad_target(holder, params)
+            if g is not None and g.numel() != 2 * C:
+                g = None
+        if g is not None:
+            dw, db = g[:C], g[C:]
+        else:
+            dw = torch.zeros(C, device=xo.device, dtype=torch.float32)
+            db = torch.zeros(C, device=xo.device, dtype=torch.float32)
+        part = torch.empty(lib.dta_ln_bwd_workspace_bytes(xo.shape[0], C) // 4, device=xo.device, dtype=torch.float32)
+        args = _lib.LnArgs(_lib.DTA_F32, xo.shape[0], C, eps, 1.0, xo.data_ptr(), C, None, 0, w32.data_ptr(), None,
+                           mean.data_ptr(), rstd.data_ptr(), dy2.data_ptr(), C, dx.data_ptr(), C, dw.data_ptr(),
+                           db.data_ptr(), part.data_ptr(), io, None, 0, None, 0,
+                           dres.data_ptr() if dres is not None else None, C, da.data_ptr(), C)
+        _lib.check(lib.dta_ln_bwd(args, _lib.stream_handle(xo.device)))
+        da_out = da.view(xshape).to(adt)
+        if g is not None:
+            hook = ctx.bound[0]["on_ready"]
+            for p in ctx.bound[1]:
+                hook(p)
+            return dx.view(xshape), da_out, None, None, None, None, None
+        return dx.view(xshape), da_out, dw.to(wdt).view(wshape), db.to(bdt).view(bshape), None, None, None
+
+
+def add_layer_norm(x: Tensor, a: Tensor, ln: "LayerNorm"):
+    """(x + a, ln(x + a)) -- a Block's residual add and the following pre-LN
+    (diff_transformer.py:121-125).  One fused pass when x is the fp32 residual stream
+    under autocast and ln emits the autocast dtype; otherwise the two ops."""
+    C = x.shape[-1]
+    if (_RES_FUSE and x.is_cuda and x.dtype == torch.float32 and isinstance(ln, LayerNorm) and ln.autocast_out
+            and torch.is_autocast_enabled("cuda") and ln.weight is not None and ln.bias is not None
+            and len(ln.normalized_shape) == 1 and C % 8 == 0 and C <= 8192 and a.shape == x.shape
+            and a.dtype in (torch.bfloat16, torch.float16)):
+        ydt = torch.get_autocast_dtype("cuda")
+        with torch.autocast("cuda", enabled=False):
+            return _AddLN.apply(x, a, ln.weight, ln.bias, ln.eps, ln._gpack, ydt)
+    xo = x + a
+    return xo, ln(xo)
+
+
+_RES_FUSE = os.environ.get("DTA_RES_FUSE", "1") != "0"        # A/B switch: 0 = add, then LayerNorm
 
 
 def group_ln_scale(x: Tensor, w: Tensor, b: Tensor, eps: float = 1e-5, out_scale: float = 1.0,

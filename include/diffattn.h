@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define DTA_ABI_VERSION 2
+#define DTA_ABI_VERSION 3
 
 enum dta_dtype { DTA_BF16 = 0, DTA_F16 = 1, DTA_F32 = 2 };
 
@@ -158,6 +158,12 @@ typedef struct dta_ln_args {
                                         with dtype = DTA_F32 and y / dy DTA_BF16 or DTA_F16 (an fp32
                                         residual stream normalised straight into the autocast
                                         dtype, and its backward from that dtype's gradient) */
+  /* residual fusion, io_dtype != 0 only (NULL = off): the pre-LN residual add of a
+   * Block (diff_transformer.py:121-125, x + attn(ln1(x)) feeding ln2) in the same pass */
+  const void* res; int64_t res_stride;   /* fwd: normalises x + res (res in the y dtype) ... */
+  float* xo; int64_t xo_stride;          /* ... and writes x + res here (fp32, required with res) */
+  const float* dres; int64_t dres_stride;  /* bwd: dx += dres (fp32 gradient of the residual branch) */
+  void* dx16; int64_t dx16_stride;       /* bwd: dx also written in the y dtype */
 } dta_ln_args;
 
 int dta_ln_fwd(const dta_ln_args* a, void* stream);

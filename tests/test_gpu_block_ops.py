@@ -250,3 +250,44 @@ def test_linear_op_matches_nn_linear(mode):
     assert lg.weight.grad.dtype == torch.float32
     assert rel_err(lg.weight.grad.cpu(), ref.weight.grad) < tol
     assert rel_err(lg.bias.grad.cpu(), ref.bias.grad) < tol
+
+
+def test_add_layer_norm_fused_equals_unfused():
+    """ops.add_layer_norm (a Block's residual add + ln2 in one pass, fp32 stream, bf16
+    branch output, bf16 LN output under autocast) gives bitwise the outputs and
+    gradients of x + a followed by the LayerNorm, and matches fp64 within bf16 tolerance."""
+    from differential_transformer_replication_amd import ops as O_
+    torch.manual_seed(6)
+    C = 1024
+    ln = O_.LayerNorm(C, autocast_out=True).to(DEV)
+    with torch.no_grad():
+        ln.weight.normal_(1.0, 0.1)
+        ln.bias.normal_(0.0, 0.1)
+    x0 = torch.randn(3, 77, C, device=DEV)
+    a0 = torch.randn(3, 77, C, device=DEV).to(torch.bfloat16)
+    gx = torch.randn(3, 77, C, device=DEV)
+    gy = torch.randn(3, 77, C, device=DEV).to(torch.bfloat16)
+    outs = []
+    for fused in (True, False):
+        O_._RES_FUSE = fused
+        x = x0.clone().requires_grad_(True)
+        a = a0.clone().requires_grad_(True)
+        ln.weight.grad = ln.bias.grad = None
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            xo, y = O_.add_layer_norm(x, a, ln)
+        assert xo.dtype == torch.float32 and y.dtype == torch.bfloat16
+        (xo * gx).sum().backward(retain_graph=True)
+        (y.float() * gy.float()).sum().backward()
+        outs.append([t.detach().clone() for t in (xo, y, x.grad, a.grad, ln.weight.grad, ln.bias.grad)])
+    O_._RES_FUSE = True
+    for u, v in zip(*outs):
+        assert torch.equal(u, v)
+    # fp64 reference of the same math
+    x64 = x0.double().requires_grad_(True)
+    a64 = a0.double().requires_grad_(True)
+    s = x64 + a64
+    y64 = F.layer_norm(s, (C,), ln.weight.double(), ln.bias.double(), ln.eps)
+    ((s * gx.double()).sum() + (y64 * gy.double()).sum()).backward()
+    assert rel_err(outs[0][1].float().cpu(), y64.detach().cpu()) < 2e-2
+    assert rel_err(outs[0][2].cpu(), x64.grad.cpu()) < 2e-2
+    assert rel_err(outs[0][3].float().cpu(), a64.grad.cpu()) < 2e-2
