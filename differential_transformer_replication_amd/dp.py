@@ -48,9 +48,12 @@ class _Bucket:
 
 class BucketedAllReduce:
     def __init__(self, module: torch.nn.Module, bucket_cap_mb: float = 64.0,
-                 process_group: Optional[dist.ProcessGroup] = None, broadcast_init: bool = True):
+                 process_group: Optional[dist.ProcessGroup] = None, broadcast_init: bool = True,
+                 reduce_single: bool = False):
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
+        # reduce_single: run the collectives even in a 1-rank group (tests of the RCCL path)
+        self._reduce = self.world > 1 or (reduce_single and dist.is_initialized())
         self.params = [p for p in module.parameters() if p.requires_grad]
         self._enabled = True
         cap = int(bucket_cap_mb * 1024 * 1024)
@@ -120,7 +123,7 @@ class BucketedAllReduce:
 
     # ----------------------------------------------------------- hooks ---
     def _on_grad(self, p: torch.nn.Parameter) -> None:
-        if not self._enabled or self.world == 1:
+        if not self._enabled or not self._reduce:
             return
         b = self._owner[id(p)]
         if p.grad is None or p.grad.data_ptr() < b.flat.data_ptr() or \
@@ -142,7 +145,7 @@ class BucketedAllReduce:
     def synchronize(self) -> None:
         """Wait for every bucket (launching any whose gradients never all arrived,
         e.g. unused parameters -- identical on every rank) and average."""
-        if self.world == 1:
+        if not self._reduce:
             return
         for b in self.buckets:
             if b.handle is None:
