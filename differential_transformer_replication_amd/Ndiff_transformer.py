@@ -182,6 +182,12 @@ class Block(nn.Module):
         x, h = ops.add_layer_norm(x, self.diff_attn(self.ln1(x), layer_idx), self.ln2)
         return x + ops.ffn(self.ffwd, h)
 
+    def forward_chained(self, x, h, layer_idx, next_ln):
+        """forward() given h = ln1(x), returning (x_out, next_ln(x_out)): both residual
+        adds fused with the LayerNorm that follows them (the model's block loop)."""
+        x, h = ops.add_layer_norm(x, self.diff_attn(h, layer_idx), self.ln2)
+        return ops.add_layer_norm(x, ops.ffn(self.ffwd, h), next_ln)
+
 
 class AlternatingDiffTransformer(nn.Module):
     """Token embeddings only (no position table), RoPE inside attention
@@ -205,9 +211,13 @@ class AlternatingDiffTransformer(nn.Module):
     def forward(self, idx, targets=None):
         B, T = idx.shape
         x = self.token_embedding_table(idx)
+        # the block loop with every residual add fused into the LayerNorm after it
+        # (ln1 of the next block, ln_f after the last); 1-based layer index (:161)
+        n = len(self.blocks)
+        h = self.blocks[0].ln1(x) if n else self.ln_f(x)
         for layer, block in enumerate(self.blocks, 1):
-            x = block(x, layer)
-        logits = self.lm_head(self.ln_f(x))
+            x, h = block.forward_chained(x, h, layer, self.blocks[layer].ln1 if layer < n else self.ln_f)
+        logits = self.lm_head(h)
         loss = None
         if targets is not None:
             logits = logits.view(B * T, -1)             # reference returns (B*T, V) with targets

@@ -147,6 +147,12 @@ class Block(nn.Module):
         x, h = ops.add_layer_norm(x, self.attn(self.ln1(x)), self.ln2)
         return x + ops.ffn(self.ffwd, h)
 
+    def forward_chained(self, x, h, next_ln):
+        """forward() given h = ln1(x), returning (x_out, next_ln(x_out)): both residual
+        adds fused with the LayerNorm that follows them (the model's block loop)."""
+        x, h = ops.add_layer_norm(x, self.attn(h), self.ln2)
+        return ops.add_layer_norm(x, ops.ffn(self.ffwd, h), next_ln)
+
 
 class StandardTransformer(nn.Module):
     """control.py:113-171."""
@@ -169,9 +175,12 @@ class StandardTransformer(nn.Module):
     def forward(self, idx, targets=None):
         B, T = idx.shape
         x = self.token_embedding_table(idx)
-        for block in self.blocks:
-            x = block(x)
-        logits = self.lm_head(self.ln_f(x))
+        # the block loop with every residual add fused into the LayerNorm after it
+        n = len(self.blocks)
+        h = self.blocks[0].ln1(x) if n else self.ln_f(x)
+        for i, block in enumerate(self.blocks):
+            x, h = block.forward_chained(x, h, self.blocks[i + 1].ln1 if i + 1 < n else self.ln_f)
+        logits = self.lm_head(h)
         loss = None
         if targets is not None:
             logits = logits.view(B * T, -1)             # reference returns (B*T, V) with targets
