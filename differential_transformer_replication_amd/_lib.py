@@ -26,7 +26,7 @@ EXPORTS = ("dta_attn_fwd", "dta_attn_bwd", "dta_attn_bwd_workspace_bytes", "dta_
            "dta_ln_fwd", "dta_ln_bwd", "dta_ln_bwd_workspace_bytes",
            "dta_rope", "dta_cast_f32", "dta_error_string", "dta_abi_version", "dta_supported",
            "dta_attn_decode", "dta_attn_decode_workspace_bytes", "dta_swiglu_fwd", "dta_swiglu_bwd",
-           "dta_accumulate_f32")
+           "dta_accumulate_f32", "dta_swiglu_bwd_workspace_bytes")
 
 
 class DtaTensor(ctypes.Structure):
@@ -41,7 +41,8 @@ class SwigluArgs(ctypes.Structure):
                 ("out", ctypes.c_void_p), ("out_stride", ctypes.c_int64),
                 ("dout", ctypes.c_void_p), ("dout_stride", ctypes.c_int64),
                 ("da", ctypes.c_void_p), ("da_stride", ctypes.c_int64),
-                ("db", ctypes.c_void_p), ("db_stride", ctypes.c_int64)]
+                ("db", ctypes.c_void_p), ("db_stride", ctypes.c_int64),
+                ("dbias", ctypes.c_void_p), ("dbias_work", ctypes.c_void_p)]
 
 
 class AttnFwdArgs(ctypes.Structure):
@@ -121,6 +122,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         lib.dta_swiglu_fwd.argtypes = [P(SwigluArgs), ctypes.c_void_p]
         lib.dta_swiglu_bwd.argtypes = [P(SwigluArgs), ctypes.c_void_p]
         lib.dta_cast_f32.argtypes = [ctypes.c_int32] * 6 + [ctypes.c_void_p, DtaTensor, ctypes.c_void_p]
+        lib.dta_swiglu_bwd_workspace_bytes.argtypes = [ctypes.c_int64, ctypes.c_int64]
+        lib.dta_swiglu_bwd_workspace_bytes.restype = ctypes.c_size_t
         lib.dta_accumulate_f32.argtypes = [ctypes.c_int32, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
                                            ctypes.c_void_p]
         lib.dta_attn_decode.argtypes = [P(DecodeArgs), ctypes.c_void_p]

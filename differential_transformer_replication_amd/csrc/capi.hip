@@ -331,7 +331,16 @@ int dta_swiglu_fwd(const dta_swiglu_args* a, void* stream) {
 int dta_swiglu_bwd(const dta_swiglu_args* a, void* stream) {
   SwigluParams p;
   if (int e = swiglu_common(a, true, p)) return e;
+  if (a->dbias) {
+    if (!aligned_ptr(a->dbias) || !aligned_ptr(a->dbias_work)) return DTA_ERR_INVALID;
+    if (a->rows == 0 || a->n == 0) return status(hipMemsetAsync(a->dbias, 0, sizeof(float) * 2 * a->n, (hipStream_t)stream));
+    return status(launch_swiglu_bias(a->dtype, p, a->dbias, a->dbias_work, (hipStream_t)stream));
+  }
   return status(launch_swiglu(a->dtype, p, true, (hipStream_t)stream));
+}
+
+size_t dta_swiglu_bwd_workspace_bytes(int64_t rows, int64_t n) {
+  return rows < 0 || n < 0 ? 0 : (size_t)swiglu_bias_work_floats(rows, n) * 4;
 }
 
 int dta_accumulate_f32(int32_t dtype, int64_t n, const void* src, float* dst, void* stream) {

@@ -119,5 +119,7 @@ struct SwigluParams {
 };
 int launch_swiglu(int dtype, const SwigluParams& p, bool bwd, hipStream_t st);
 int launch_accumulate(int dtype, int64_t n, const void* src, float* dst, hipStream_t st);
+int launch_swiglu_bias(int dtype, const SwigluParams& p, float* dbias, float* work, hipStream_t st);
+int64_t swiglu_bias_work_floats(int64_t rows, int64_t n);
 
 }  // namespace dta

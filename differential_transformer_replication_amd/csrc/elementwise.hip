@@ -699,6 +699,65 @@ __global__ __launch_bounds__(256) void swiglu_bwd_kernel(SwigluParams p) {
   }
 }
 
+// Backward with the column sums of dA | dB (the packed gate / xform Linears' bias
+// gradient, diff_transformer.py:95-105 under autocast: the sum over rows of the
+// gradients as stored): each block owns 2048 columns x SWIGLU_RB rows, sums the
+// rounded values in fp32 and writes its partials [row block][2n]; a second kernel adds
+// the row blocks in a fixed order (bitwise reproducible, no atomics).
+constexpr int SWIGLU_RB = 128;
+template <class E>
+__global__ __launch_bounds__(256) void swiglu_bwd_bias_kernel(SwigluParams p, float* part) {
+  const int64_t c = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
+  if (c >= p.n) return;
+  const int64_t r0 = (int64_t)blockIdx.y * SWIGLU_RB, r1 = min(r0 + SWIGLU_RB, p.rows);
+  float sa[8], sb[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { sa[j] = 0.f; sb[j] = 0.f; }
+#pragma unroll 2
+  for (int64_t r = r0; r < r1; ++r) {
+    float a[8], b[8], d[8], da[8], db[8];
+    ld8<E>(reinterpret_cast<const E*>(p.a) + r * p.as + c, a);
+    ld8<E>(reinterpret_cast<const E*>(p.b) + r * p.bs + c, b);
+    ld8<E>(reinterpret_cast<const E*>(p.dout) + r * p.dos + c, d);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float sg;
+      const float sl = silu_f<E>(a[j], sg);
+      db[j] = (float)(E)(d[j] * sl);
+      da[j] = (float)(E)(d[j] * b[j] * (sg * (1.f + a[j] * (1.f - sg))));
+      sa[j] += da[j];
+      sb[j] += db[j];
+    }
+    st8<E>(reinterpret_cast<E*>(p.da) + r * p.das + c, da);
+    st8<E>(reinterpret_cast<E*>(p.db) + r * p.dbs + c, db);
+  }
+  float* pa = part + (int64_t)blockIdx.y * 2 * p.n + c;
+  st8<float>(pa, sa);
+  st8<float>(pa + p.n, sb);
+}
+__global__ __launch_bounds__(256) void swiglu_bias_reduce_kernel(const float* part, int nblk, int64_t n2, float* out) {
+  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j >= n2) return;
+  float s = 0.f;
+  for (int b = 0; b < nblk; ++b) s += part[(int64_t)b * n2 + j];
+  out[j] = s;
+}
+int64_t swiglu_bias_work_floats(int64_t rows, int64_t n) { return (rows + SWIGLU_RB - 1) / SWIGLU_RB * 2 * n; }
+
+int launch_swiglu_bias(int dtype, const SwigluParams& p, float* dbias, float* work, hipStream_t st) {
+  const int nblk = (int)((p.rows + SWIGLU_RB - 1) / SWIGLU_RB);
+  const dim3 g((unsigned)((p.n / 8 + 255) / 256), (unsigned)nblk);
+  switch (dtype) {
+    case 0: hipLaunchKernelGGL(swiglu_bwd_bias_kernel<__bf16>, g, dim3(256), 0, st, p, work); break;
+    case 1: hipLaunchKernelGGL(swiglu_bwd_bias_kernel<_Float16>, g, dim3(256), 0, st, p, work); break;
+    case 2: hipLaunchKernelGGL(swiglu_bwd_bias_kernel<float>, g, dim3(256), 0, st, p, work); break;
+    default: return -1;
+  }
+  hipLaunchKernelGGL(swiglu_bias_reduce_kernel, dim3((unsigned)((2 * p.n + 255) / 256)), dim3(256), 0, st, work, nblk,
+                     2 * p.n, dbias);
+  return (int)hipGetLastError();
+}
+
 int launch_swiglu(int dtype, const SwigluParams& p, bool bwd, hipStream_t st) {
   const int64_t items = p.rows * (p.n / 8);
   if (items == 0) return 0;

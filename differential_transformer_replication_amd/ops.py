@@ -346,6 +346,7 @@ def add_layer_norm(x: Tensor, a: Tensor, ln: "LayerNorm"):
 
 
 _RES_FUSE = os.environ.get("DTA_RES_FUSE", "1") != "0"        # A/B switch: 0 = add, then LayerNorm
+_SWIGLU_BIAS = os.environ.get("DTA_SWIGLU_BIAS", "1") != "0"   # A/B switch: 0 = bias gradient by torch's sum
 
 
 def group_ln_scale(x: Tensor, w: Tensor, b: Tensor, eps: float = 1e-5, out_scale: float = 1.0,
@@ -428,7 +429,8 @@ def swiglu(a: Tensor, b: Tensor) -> Tensor:
     return _SwiGLU.apply(a, b)
 
 
-def _swiglu_launch(y2: Tensor, n: int, out: Optional[Tensor], dout: Optional[Tensor], dy: Optional[Tensor]):
+def _swiglu_launch(y2: Tensor, n: int, out: Optional[Tensor], dout: Optional[Tensor], dy: Optional[Tensor],
+                   dbias: Optional[Tensor] = None):
     """dta_swiglu over the column halves of a packed (rows, 2n) projection: a = y2[:, :n],
     b = y2[:, n:]; forward writes ``out`` (rows, n), backward writes da | db into the halves
     of ``dy`` (rows, 2n)."""
@@ -440,8 +442,14 @@ def _swiglu_launch(y2: Tensor, n: int, out: Optional[Tensor], dout: Optional[Ten
                              None, 0, None, 0, None, 0)
         _lib.check(lib.dta_swiglu_fwd(sa, _lib.stream_handle(y2.device)))
     else:
+        work = None
+        if dbias is not None:
+            work = torch.empty(lib.dta_swiglu_bwd_workspace_bytes(rows, n) // 4 + 4, device=y2.device,
+                               dtype=torch.float32)
         sa = _lib.SwigluArgs(_lib.dtype_code(y2.dtype), rows, n, a, w, b, w, None, 0, dout.data_ptr(), n,
-                             dy.data_ptr(), w, dy.data_ptr() + n * es, w)
+                             dy.data_ptr(), w, dy.data_ptr() + n * es, w,
+                             dbias.data_ptr() if dbias is not None else None,
+                             work.data_ptr() if work is not None else None)
         _lib.check(lib.dta_swiglu_bwd(sa, _lib.stream_handle(y2.device)))
 
 
@@ -479,11 +487,14 @@ class _PackedSwiGLU(torch.autograd.Function):
         n = ctx.n
         d2 = dout.to(y2.dtype).contiguous().view(-1, n)
         dy = torch.empty_like(y2)
-        _swiglu_launch(y2, n, None, d2, dy)
+        # the bias gradient (column sums of dA | dB as stored) comes out of the same pass
+        db = torch.empty(2 * n, device=y2.device, dtype=torch.float32) if _SWIGLU_BIAS else None
+        _swiglu_launch(y2, n, None, d2, dy, db)
         with torch.autocast("cuda", enabled=False):
             dx = (dy @ wc).view(*xc.shape[:-1], xc.shape[-1]).to(ctx.x_dtype) if ctx.needs_input_grad[0] else None
             dw = packing.weight_grad(dy, xc.reshape(-1, xc.shape[-1]))
-            db = dy.sum(0)
+            if db is None:
+                db = dy.sum(0)
         if ctx.holders is not None and all(ctx.needs_input_grad[5:]):
             wh, bh = ctx.holders
             gw = packing._grad_target(wh, ctx.params[:2])

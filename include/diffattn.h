@@ -236,9 +236,14 @@ typedef struct {
   const void* dout; int64_t dout_stride;
   void* da; int64_t da_stride;
   void* db; int64_t db_stride;
+  /* backward, optional (ABI 3): with dbias, also the column sums of dA | dB as stored
+   * (fp32 [2n]: the gate / xform Linears' bias gradient), through dbias_work
+   * (dta_swiglu_bwd_workspace_bytes), summed in a fixed order */
+  float* dbias; float* dbias_work;
 } dta_swiglu_args;
 int dta_swiglu_fwd(const dta_swiglu_args* a, void* stream);
 int dta_swiglu_bwd(const dta_swiglu_args* a, void* stream);
+size_t dta_swiglu_bwd_workspace_bytes(int64_t rows, int64_t n);
 
 /* dst[i] += (float)src[i], i < n: gradient accumulation of a bf16/fp16/fp32 weight
  * gradient into fp32 master-gradient storage (the training step's packed projection

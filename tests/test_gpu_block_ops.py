@@ -291,3 +291,21 @@ def test_add_layer_norm_fused_equals_unfused():
     assert rel_err(outs[0][1].float().cpu(), y64.detach().cpu()) < 2e-2
     assert rel_err(outs[0][2].cpu(), x64.grad.cpu()) < 2e-2
     assert rel_err(outs[0][3].float().cpu(), a64.grad.cpu()) < 2e-2
+
+
+@pytest.mark.parametrize("rows,n", [(300, 256), (4096, 1024), (1, 64)])
+def test_swiglu_bias_gradient_pass(rows, n):
+    """dta_swiglu_bwd with dbias: dA | dB as the plain backward writes them, plus their
+    column sums (the packed gate / xform bias gradient) summed in a fixed order."""
+    from differential_transformer_replication_amd import ops as O_
+    gen = torch.Generator().manual_seed(rows + n)
+    y2 = (torch.randn(rows, 2 * n, generator=gen) * 2).to(torch.bfloat16).to(DEV)
+    d2 = torch.randn(rows, n, generator=gen).to(torch.bfloat16).to(DEV)
+    dy_ref, dy = torch.empty_like(y2), torch.empty_like(y2)
+    O_._swiglu_launch(y2, n, None, d2, dy_ref)
+    db = torch.empty(2 * n, device=DEV)
+    O_._swiglu_launch(y2, n, None, d2, dy, db)
+    torch.cuda.synchronize()
+    assert torch.equal(dy, dy_ref)
+    ref = dy_ref.double().sum(0)
+    assert rel_err(db.cpu(), ref.cpu()) < 1e-5
