@@ -529,16 +529,22 @@ template <class E> struct FwdTile { static constexpr int BN = 64; };
 template <> struct FwdTile<float> { static constexpr int BN = 32; };
 
 // dv chunk per forward workgroup: keep N * DVC/2 accumulator VGPRs <= 128
-template <int N, int DV>
+#ifndef DTA_FWD_FULLDV   // N * dv / 2 <= this many accumulator VGPRs: one workgroup takes the whole dv
+#define DTA_FWD_FULLDV 192
+#endif
+template <int N, int DV, bool B16 = true>
 struct FwdChunk {
-  static constexpr int cap = (256 / N) / 32 * 32;
+  // 16-bit: N = 3 at dv = 128 takes the whole dv in one (one-wave-per-SIMD) workgroup
+  // instead of two dv chunks that each redo QK^T and the softmax (fwd 0.523 -> 0.470 ms
+  // at cfg3's shape); N = 4 spills that way
+  static constexpr int cap = (B16 && N * DV / 2 <= DTA_FWD_FULLDV) ? DV : (256 / N) / 32 * 32;
   static constexpr int DVC = DV <= cap ? DV : (cap >= 128 && DV % 128 == 0 ? 128 : (cap >= 64 ? 64 : 32));
 };
 
 template <class E, int HS, int N, int DVC, int NW, bool QREG, int QRH = 0>
 struct FwdCfg {
   // QRH > 0 (paired plan): the first QRH branches' Q rows stay in registers
-  static constexpr bool PAIR = DTA_FWD_PAIR && NW == 4 && !QREG && sizeof(E) == 2;
+  static constexpr bool PAIR = DTA_FWD_PAIR && NW == 4 && !QREG && sizeof(E) == 2 && N * DVC / 2 <= 128;
   static constexpr int BN = (PAIR && QRH == 0) ? 32 : FwdTile<E>::BN;
   static constexpr int BM = NW * 32;
   static constexpr int nQ = QREG ? 0 : (N - QRH) * BM * HS;
@@ -556,7 +562,7 @@ struct FwdCfg {
 // NP: no paired plan (the dropout instantiations: their extra registers spill it)
 template <class E, int HS, int N, int DV = 2 * HS, bool NP = false>
 struct FwdPick {
-  static constexpr int DVC = FwdChunk<N, DV>::DVC;
+  static constexpr int DVC = FwdChunk<N, DV, sizeof(E) == 2>::DVC;
   static constexpr int LIM = 160 * 1024;
   static constexpr int NWMAX = sizeof(E) == 2 ? 8 : 4;
   // widest workgroup with Q in LDS, else Q in registers
