@@ -1393,7 +1393,7 @@ void attn_dq_kernel(BwdParams p) {
   const int ntiles = (kend + BN - 1) / BN;
   using KR = KvRing<E, HS, N, DV, BN, NW>;
   static_assert(!SRD || HSP == HS, "descriptor staging needs unpadded K rows");
-  constexpr bool PRE = DTA_DQ_PREOFF && SRD;     // per-lane DMA source offsets computed once
+  constexpr bool PRE = DTA_DQ_PREOFF && SRD && !DROP;  // DMA source offsets computed once (dropout: fewer spills without)
   uint32_t doff[PRE ? KR::MYP : 1];
   if constexpr (PRE) KR::offsets(p.k.st, p.k.si, p.v.st, wave, lane, doff);
   auto stage_kv = [&](int kt, int buf) {
@@ -1487,7 +1487,7 @@ void attn_dq_kernel(BwdParams p) {
   // XA (see attn_dkdv_kernel): the ring slot's base added once per step, the k-step XOR after it
   constexpr int XMAX = 32 * ((NSV > NSQ ? NSV : NSQ) - 1) + 64 * (NHB - 1) + 32;
   constexpr int XM = XMAX < 256 ? 256 : (XMAX < 512 ? 512 : 1024);
-  constexpr bool XA = DTA_DQ_LBASE && SRD && sizeof(E) == 2 && (CF::nQ * (int)sizeof(E)) % XM == 0 &&
+  constexpr bool XA = DTA_DQ_LBASE && !DROP && SRD && sizeof(E) == 2 && (CF::nQ * (int)sizeof(E)) % XM == 0 &&
                       (CF::nK * (int)sizeof(E)) % XM == 0 && (CF::nV * (int)sizeof(E)) % XM == 0;
   if constexpr (sizeof(E) == 2) {
     LrV = row_lane<VI::ROWB>(lane); LrK = row_lane<KI::ROWB>(lane); LrQ = row_lane<QI::ROWB>(lane);
@@ -1498,7 +1498,7 @@ void attn_dq_kernel(BwdParams p) {
     // keep lane-derived addresses loop-variant: recomputed per tile instead of
     // hoisted into (spilled) registers across the whole loop
     asm volatile("" : "+v"(lane));
-    if constexpr (DTA_DQ_LBASE && sizeof(E) == 2) {
+    if constexpr (DTA_DQ_LBASE && !DROP && sizeof(E) == 2) {
       asm volatile("" : "+v"(LrV), "+v"(LrK), "+v"(LtK));
       if constexpr (QI::ROWB == KI::ROWB) LrQ = LrK;
       else asm volatile("" : "+v"(LrQ));
