@@ -145,7 +145,9 @@ def _pmc_traffic(kernel, shape=DEFAULT_SHAPE):
     per the gfx950 correction).  Summaries without a "shape" field were all taken
     on the default cfg2 command.  (None, None) when no summary matches."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))   # rNN_vM: newest last
+    import re
+    nat = lambda f: [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", os.path.basename(f))]
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")), key=nat)  # rNN_vM: newest last
     for f in reversed(files):
         try:
             with open(f) as fh:
