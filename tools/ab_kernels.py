@@ -101,9 +101,14 @@ def main():
     torch.cuda.synchronize()
     base = builds[0][0]
     res = {n: {"fwd": [], "dq": [], "dkdv": []} for n, _ in builds}
-    for _ in range(args.rounds):
-        for name, _ in builds:
+    # the order rotates every round and each block's first launch is untimed: a fixed
+    # order read the first build ~0.1 ms/step slow (profiles/r02_ab_sched_strategy.json)
+    for r in range(args.rounds):
+        for name, _ in builds[r % len(builds):] + builds[:r % len(builds)]:
             for w in ("fwd", "dq", "dkdv"):
+                if w == "dq":
+                    run(name, "pre")
+                run(name, w)
                 ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                       for _ in range(args.reps)]
                 for e0, e1 in ev:
