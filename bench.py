@@ -138,14 +138,25 @@ def shape_key(B, H, hs, N, T, dv) -> str:
     return f"B{B}_H{H}_hs{hs}_N{N}_T{T}_dv{dv}"
 
 
+def lib_sha() -> str:
+    """First 16 hex digits of sha256(libdiffattn.so): the kernel build being run."""
+    import hashlib
+    path = os.path.join(ROOT, "differential_transformer_replication_amd", "lib", "libdiffattn.so")
+    with open(path, "rb") as fh:
+        return hashlib.sha256(fh.read()).hexdigest()[:16]
+
+
 def _pmc_traffic(kernel, shape=DEFAULT_SHAPE):
     """HBM bytes per launch of ``kernel`` at workload ``shape`` from the newest
     committed PMC summary for that shape (profiles/*_pmc_traffic.json, written
     from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE doubled
-    per the gfx950 correction).  Summaries without a "shape" field were all taken
-    on the default cfg2 command.  (None, None) when no summary matches."""
+    per the gfx950 correction), and only one taken on the kernel build this run
+    loads (its ``lib_sha``): counters of an older build are never paired with this
+    build's timings.  Summaries without a "shape" field were all taken on the
+    default cfg2 command.  (None, None) when no summary matches."""
     import glob
     import re
+    cur = lib_sha()
     nat = lambda f: [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", os.path.basename(f))]
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")), key=nat)  # rNN_vM: newest last
     for f in reversed(files):
@@ -153,7 +164,7 @@ def _pmc_traffic(kernel, shape=DEFAULT_SHAPE):
             with open(f) as fh:
                 d = json.load(fh)
             legacy = ("decode_" if kernel.startswith("decode") else "") + DEFAULT_SHAPE
-            if d.get("shape", legacy) != shape:
+            if d.get("shape", legacy) != shape or d.get("lib_sha") != cur:
                 continue
             k = d["kernels"].get(kernel)
         except (OSError, ValueError, KeyError):
@@ -218,37 +229,46 @@ def control_fused_bench(B, H, hs, T, steps, warmup):
     return sec * 1e3, f / sec / 1e12
 
 
-def kernel_bench(args, world, rank):
-    from differential_transformer_replication_amd import ops
+def _coefficients(H, N, hs, dev):
+    """Seeded branch coefficients: lambda_* ~ N(0, 0.1) at layer 3."""
     from differential_transformer_replication_amd.diff_transformer import _layer_lambda_coef
     from differential_transformer_replication_amd.Ndiff_transformer import alternating_coefficients
     from differential_transformer_replication_amd._compat import lambda_init_value
-    B, H, hs, N, T = args.batch, args.heads, args.head_size, args.n_terms, args.seq
-    dv = 2 * hs
+    g1 = torch.Generator(device=dev).manual_seed(1)
+    if N == 1:
+        return torch.ones(H, 1, device=dev)
+    if N == 2:
+        lam = [torch.randn(H, hs, device=dev, generator=g1) * 0.1 for _ in range(4)]
+        return _layer_lambda_coef(*lam, lambda_init_value(3, None))
+    lqs, lks = (torch.randn(H, N, hs, device=dev, generator=g1) * 0.1 for _ in range(2))   # Ndiff_transformer.py:79-93
+    return alternating_coefficients(lqs, lks, float(lambda_init_value(3, None)))
+
+
+def core_run(B, H, hs, N, T, steps, warmup, world=1, rank=0, dv=None):
+    """Forward + backward of the fused attention core (bf16, causal, synthetic N(0,1)
+    inputs resident in HBM) ``steps`` times after ``warmup``; the wall time of the
+    timed region (barrier + synchronize on both sides, MAX over ranks) and every
+    kernel's mean HIP-event time with its algorithmic TFLOP/s."""
+    from differential_transformer_replication_amd import ops
+    dv = 2 * hs if dv is None else dv
     dev = torch.device("cuda", torch.cuda.current_device())
     W = ops.packed_width(H, N, hs, dv)
     g = torch.Generator(device=dev).manual_seed(0 + rank)
     qkv = torch.randn(B, T, W, device=dev, dtype=torch.bfloat16, generator=g).requires_grad_(True)
     do = torch.randn(B, T, H * dv, device=dev, dtype=torch.bfloat16, generator=g)
-    g1 = torch.Generator(device=dev).manual_seed(1)
-    if N == 2:
-        lam = [torch.randn(H, hs, device=dev, generator=g1) * 0.1 for _ in range(4)]
-        coef = _layer_lambda_coef(*lam, lambda_init_value(3, None))
-    else:                                        # N-term alternating coefficients (Ndiff_transformer.py:79-93)
-        lqs, lks = (torch.randn(H, N, hs, device=dev, generator=g1) * 0.1 for _ in range(2))
-        coef = alternating_coefficients(lqs, lks, float(lambda_init_value(3, None)))
+    coef = _coefficients(H, N, hs, dev)
 
     def step():
         qkv.grad = None
-        out = ops.diff_attention(qkv, coef, H, N, hs)
+        out = ops.diff_attention(qkv, coef, H, N, hs, dv=dv)
         out.backward(do)
 
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
     _sync(world)
     ops.TIMER.start()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         step()
     _sync(world)
     el = time.perf_counter() - t0
@@ -257,8 +277,6 @@ def kernel_bench(args, world, rank):
     kt = ops.TIMER.mean_ms()
     f_fwd = float(B) * H * T * T * (N * hs + dv)
     f_bwd = 2 * f_fwd
-    ms = el / args.steps * 1e3
-    value = world * (f_fwd + f_bwd) / (el / args.steps) / 1e12
     # per-kernel algorithmic FLOPs: the forward does F_fwd; the backward's 2*F_fwd is split by
     # its two kernels' products: dq (dQ = dS K) and dkdv (dV = P^T dO, dK = dS^T Q, dP = dO V^T)
     dq_share = N * hs / (2.0 * (N * hs + dv))
@@ -266,6 +284,16 @@ def kernel_bench(args, world, rank):
     kernels = {}
     for name, (t, n) in kt.items():
         kernels[name] = {"ms": round(t, 4), "launches": n, "alg_tflops": round(flops[name] / t / 1e9, 2)}
+    del qkv, do
+    return el / steps, f_fwd + f_bwd, kernels
+
+
+def kernel_bench(args, world, rank):
+    B, H, hs, N, T = args.batch, args.heads, args.head_size, args.n_terms, args.seq
+    dv = 2 * hs
+    sec, flop, kernels = core_run(B, H, hs, N, T, args.steps, args.warmup, world, rank)
+    ms = sec * 1e3
+    value = world * flop / sec / 1e12
     dom = max(kernels, key=lambda k: kernels[k]["ms"])
     achieved = kernels[dom]["alg_tflops"]
     traffic, traffic_src = args.traffic, None
@@ -287,6 +315,7 @@ def kernel_bench(args, world, rank):
         "roofline": {"bound": "mfma", "kernel": dom, "achieved": achieved, "peak": PEAK_BF16_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
                      "traffic": traffic, "traffic_source": traffic_src},
+        "lib_sha": lib_sha(),
     }
     if args.control and rank == 0:
         # control.py standard attention at equal F_fwd: 2*H heads of width hs, dv = hs (train.py:226)
@@ -302,6 +331,40 @@ def kernel_bench(args, world, rank):
                                          "ms_per_step": round(cms, 4), "alg_tflops": round(ctf, 2),
                                          "diff_over_control_time": round(ms / cms, 3)}}
     return res
+
+
+def configs_leg(args):
+    """BASELINE configs[2] and [4] in the default line (one GPU, rank 0 only, short runs):
+      cfg3  AlternatingDiffTransformer(12000, 768, 6, 10, 2048, n_terms=3 / 4) training step
+            (bf16 autocast, micro-batch 16 x 2048): tokens/s and MFU, plus the attention
+            core alone at that shape (B=16, H=6, hs=64, T=2048) with every kernel's
+            algorithmic TFLOP/s;
+      cfg5  the long-context core, B=1, H=16, hs=128 (dv=256), T=32768, N=2, against
+            control.py's standard attention on the SAME kernels (N=1, coef 1, H=32,
+            hs=dv=128: equal algorithmic FLOPs, train.py:226's n_head*2)."""
+    from differential_transformer_replication_amd.train import train_bench
+    out = {}
+    for n in (3, 4):
+        torch.cuda.empty_cache()
+        r = train_bench(argparse.Namespace(steps=args.cfg_steps, warmup=2, model="ndiff", n_terms=n,
+                                           device="cuda"), 1, 0)
+        torch.cuda.empty_cache()
+        sec, flop, kernels = core_run(16, 6, 64, n, 2048, args.cfg_steps, 2)
+        out[f"cfg3_n{n}"] = {"train_tokens_per_s": r["value"], "train_ms_per_step": r["ms_per_step"],
+                             "mfu": r.get("mfu"), "params": r["config"]["params"],
+                             "core": {"shape": "B=16 H=6 hs=64 dv=128 T=2048 bf16 causal", "ms_per_step": round(
+                                 sec * 1e3, 4), "alg_tflops": round(flop / sec / 1e12, 2), "kernels": kernels}}
+    torch.cuda.empty_cache()
+    sec, flop, kernels = core_run(1, 16, 128, 2, 32768, max(2, args.cfg_steps // 2), 1)
+    torch.cuda.empty_cache()
+    csec, cflop, ckernels = core_run(1, 32, 128, 1, 32768, max(2, args.cfg_steps // 2), 1, dv=128)
+    out["cfg5"] = {"diff": {"shape": "B=1 H=16 hs=128 dv=256 N=2 T=32768 bf16 causal", "ms_per_step": round(sec * 1e3, 3),
+                            "alg_tflops": round(flop / sec / 1e12, 2), "kernels": kernels},
+                   "control_same_kernel": {"shape": "B=1 H=32 hs=dv=128 N=1 T=32768 bf16 causal (control.py:38-63)",
+                                           "ms_per_step": round(csec * 1e3, 3),
+                                           "alg_tflops": round(cflop / csec / 1e12, 2), "kernels": ckernels},
+                   "diff_over_control_time": round(sec / csec, 3)}
+    return out
 
 
 def decode_bench(args, world, rank):
@@ -446,6 +509,9 @@ def run(args):
         res = kernel_bench(args, world, rank)
         if rank == 0 and args.hbm:
             res["hbm_kernels"] = hbm_bench()
+        if world == 1 and args.configs and args.cfg_steps > 0:
+            torch.cuda.empty_cache()
+            res["configs"] = configs_leg(args)
         if args.train_steps > 0:
             if train is None:
                 torch.cuda.empty_cache()
@@ -505,6 +571,9 @@ def main():
                     help="kernel mode: timed steps of the cfg4 DP training leg (0 = skip)")
     ap.add_argument("--train-warmup", type=int, default=3)
     ap.add_argument("--no-hbm", dest="hbm", action="store_false", help="kernel mode: skip the LN / RoPE timings")
+    ap.add_argument("--no-configs", dest="configs", action="store_false",
+                    help="kernel mode: skip the cfg3 / cfg5 legs (one GPU only)")
+    ap.add_argument("--cfg-steps", type=int, default=4, help="timed steps of each cfg3 / cfg5 leg")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--traffic", type=float, default=None,
                     help="HBM bytes per dominant-kernel launch from rocprofv3 PMC (profiles/)")

@@ -36,7 +36,7 @@ from . import packing
 
 
 class _Bucket:
-    __slots__ = ("params", "flat", "pending", "handle", "size")
+    __slots__ = ("params", "flat", "pending", "handle", "size", "seen")
 
     def __init__(self, params: List[torch.nn.Parameter], flat: torch.Tensor):
         self.params = params
@@ -44,6 +44,12 @@ class _Bucket:
         self.size = len(params)
         self.pending = self.size
         self.handle = None
+        self.seen: set = set()          # ids of the parameters reported since the last reset
+
+    def reset(self) -> None:
+        self.pending = self.size
+        self.handle = None
+        self.seen.clear()
 
 
 class BucketedAllReduce:
@@ -108,8 +114,13 @@ class BucketedAllReduce:
             self.buckets.append(b)
             for p in g:
                 self._owner[id(p)] = b
+        # A packed group reports its parameters itself (packing.bind_grad) and returns None
+        # gradients to autograd -- whose post-accumulate hooks still fire, with nothing
+        # accumulated: hooking those parameters too would count every one of them twice
+        # and launch a bucket before the rest of its gradients are in.
         for p in self.params:
-            p.register_post_accumulate_grad_hook(self._on_grad)
+            if id(p) not in pack_of:
+                p.register_post_accumulate_grad_hook(self._on_grad)
         for holder, pp in packs:
             b = self._owner[id(pp[0])]
             start = pp[0].grad.data_ptr() - b.flat.data_ptr()
@@ -122,14 +133,27 @@ class BucketedAllReduce:
                     dist.broadcast(p.data, src=0, group=self.pg)
 
     # ----------------------------------------------------------- hooks ---
+    def _is_view(self, p: torch.nn.Parameter) -> bool:
+        b = self._owner.get(id(p))
+        if b is None or p.grad is None:
+            return False
+        lo = b.flat.data_ptr()
+        return lo <= p.grad.data_ptr() < lo + b.flat.numel() * 4
+
     def _on_grad(self, p: torch.nn.Parameter) -> None:
         if not self._enabled or not self._reduce:
-            return
-        b = self._owner[id(p)]
-        if p.grad is None or p.grad.data_ptr() < b.flat.data_ptr() or \
-                p.grad.data_ptr() >= b.flat.data_ptr() + b.flat.numel() * 4:
+            return          # (world 1: a replaced .grad falls back to per-parameter grads;
+                            # clip_grad_norm_ then checks the views itself)
+        if not self._is_view(p):
             raise RuntimeError("parameter gradient is no longer a view of its bucket "
                                "(use BucketedAllReduce.zero_grad, not set_to_none)")
+        b = self._owner[id(p)]
+        # every parameter reports exactly once per synchronised backward, and a bucket
+        # launches only once all of them are in: an early or repeated report (a backward
+        # path calling the hook itself) would otherwise all-reduce partial gradients
+        if id(p) in b.seen or b.pending <= 0:
+            raise RuntimeError("gradient reported twice to its DP bucket in one backward")
+        b.seen.add(id(p))
         b.pending -= 1
         if b.pending == 0:
             b.handle = dist.all_reduce(b.flat, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
@@ -154,14 +178,14 @@ class BucketedAllReduce:
         for b in self.buckets:
             b.handle.wait()
             b.flat.mul_(inv)
-            b.handle = None
-            b.pending = b.size
+            b.reset()
 
     def clip_grad_norm_(self, max_norm: float) -> torch.Tensor:
         """torch.nn.utils.clip_grad_norm_(params, max_norm) (train.py:273) over the flat
         buckets the parameters' gradients are views of: the same L2 norm and scale,
         computed with one norm and one multiply per bucket instead of one per parameter."""
-        if any(p.grad is None or id(p) not in self._owner for p in self.params):
+        # the bucket form only while every gradient still is a view of its bucket
+        if not all(self._is_view(p) for p in self.params):
             return torch.nn.utils.clip_grad_norm_(self.params, max_norm)
         flats = [b.flat for b in self.buckets]
         total = torch.linalg.vector_norm(torch.stack(torch._foreach_norm(flats, 2.0)), 2.0)
@@ -172,5 +196,4 @@ class BucketedAllReduce:
     def zero_grad(self) -> None:
         for b in self.buckets:
             b.flat.zero_()
-            b.pending = b.size
-            b.handle = None
+            b.reset()

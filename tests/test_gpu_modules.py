@@ -91,14 +91,39 @@ def test_module_bf16_autocast(golden, prefix):
         # fused path rounds the per-branch outputs O_i that delta_i = <dO, O_i> is formed from).
         ref_err = _reference_bf16_grad_errors(case, g)
         named = dict(m.named_parameters())
+        log = []
         for k, ref in g.grads().items():
             got = named[k].grad
             assert got is not None, (case, k)
             if float(np.abs(ref).max()) == 0.0:
                 assert float(got.abs().max()) < 1e-4, (case, k)
-            else:
-                bar = max(BF16_TOL, 2.0 * ref_err[k])
-                assert rel_err(got, ref) < bar, (case, k, rel_err(got, ref), ref_err[k])
+                continue
+            err = rel_err(got, ref)
+            # only the lambda vectors may exceed the north star's 2e-2 (reason above): their
+            # bar is 2x the reference algorithm's own bf16 error; every other gradient is held to 2e-2
+            loose = any(t in k for t in BF16_LOOSE)
+            bar = max(BF16_TOL, 2.0 * ref_err[k]) if loose else BF16_TOL
+            log.append({"case": case, "param": k, "err": err, "ref_alg_bf16_err": ref_err[k], "bar": bar,
+                        "over_2e-2": err >= BF16_TOL})
+            assert err < bar, (case, k, err, ref_err[k])
+        _log_errors(f"bf16_grad_errors_{prefix}", log)
+
+
+# parameter-name fragments whose bf16 gradient may exceed 2e-2 (test_module_bf16_autocast):
+# d lambda_* = exp(lq*lk) lk / hs * d(coef), and d(coef) = sum over (b, t) of <dO, O_i>, a sum
+# with heavy cancellation whose terms carry bf16 rounding
+BF16_LOOSE = ("lambda_q", "lambda_k")
+
+
+def _log_errors(name, rows):
+    """Every gradient's error and bar, for the run record (DTA_TEST_LOG_DIR, when set)."""
+    import json
+    d = os.environ.get("DTA_TEST_LOG_DIR")
+    if d:
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, name + ".json"), "a") as f:
+            for r in rows:
+                f.write(json.dumps(r) + "\n")
 
 
 def _reference_bf16_grad_errors(case, g):

@@ -192,30 +192,38 @@ def _sample_rows(T, n, seed):
     return sorted({r for r in fixed + rnd if 0 <= r < T})
 
 
-def _rows_reference(q, k, v, coef, rows, do_rows):
+def _rows_reference(q, k, v, coef, rows, do_rows, freqs_c=None):
     """fp64 restatement of diff_core (diff_transformer.py:57-72 / Ndiff_transformer.py:
     102-125) for the query rows ``rows`` of ONE (b, h) over the full key range.
     q, k: (T, N, hs); v: (T, dv); coef (N,); do_rows (R, dv).  Returns out_R and the
     gradients of sum(out_R * do_R) w.r.t. q (rows only), k, v and coef -- equal to the
-    full problem's gradients when dO is zero on every other row."""
+    full problem's gradients when dO is zero on every other row.  With ``freqs_c`` every
+    Q_i / K_i is rotated first (apply_rotary_emb, Ndiff_transformer.py:11-22, 104-109) and
+    the gradients are w.r.t. the unrotated projections, as the kernels return them."""
     T, N, hs = k.shape
     q = q.double().requires_grad_(True)
     k = k.double().requires_grad_(True)
     v = v.double().requires_grad_(True)
     c = coef.double().requires_grad_(True)
+    qr, kr = q, k
+    if freqs_c is not None:
+        qr = _rope64(q.transpose(0, 1), freqs_c).transpose(0, 1)      # (N, T, hs) rows -> (T, N, hs)
+        kr = _rope64(k.transpose(0, 1), freqs_c).transpose(0, 1)
     r = torch.tensor(rows)
     keep = torch.arange(T)[None, :] <= r[:, None]                       # causal: key <= query
     out = 0
     for i in range(N):
-        s = (q[r, i] @ k[:, i].t()) / math.sqrt(hs)
+        s = (qr[r, i] @ kr[:, i].t()) / math.sqrt(hs)
         a = torch.softmax(s.masked_fill(~keep, float("-inf")), dim=-1)
         out = out + c[i] * (a @ v)
     (out * do_rows.double()).sum().backward()
     return out.detach(), q.grad, k.grad, v.grad, c.grad
 
 
-def _long_case(B, H, N, hs, T, pairs, n_rows, dtype=torch.bfloat16, seed=0):
+def _long_case(B, H, N, hs, T, pairs, n_rows, dtype=torch.bfloat16, seed=0, rope=False):
     ops = _ops()
+    freqs_c = orc.precompute_freqs_cis(hs, T) if rope else None
+    freqs = torch.view_as_real(freqs_c).contiguous().to(DEV) if rope else None
     dv = 2 * hs
     W = ops.packed_width(H, N, hs, dv)
     nq = H * N * hs
@@ -231,7 +239,7 @@ def _long_case(B, H, N, hs, T, pairs, n_rows, dtype=torch.bfloat16, seed=0):
         do[b, r, h] = torch.randn(len(r), dv, device=DEV, generator=g).to(dtype)
     xg = qkv.clone().requires_grad_(True)
     cg = coef.clone().requires_grad_(True)
-    out = ops.diff_attention(xg, cg, H, N, hs)
+    out = ops.diff_attention(xg, cg, H, N, hs, freqs)
     out.backward(do.view(B, T, H * dv))
     torch.cuda.synchronize()
     tol = TOL[dtype]
@@ -243,7 +251,7 @@ def _long_case(B, H, N, hs, T, pairs, n_rows, dtype=torch.bfloat16, seed=0):
         k = x[:, nq:2 * nq].view(T, H, N, hs)[:, h]
         v = x[:, 2 * nq:].view(T, H, dv)[:, h]
         d_r = do[b, rr, h].float().cpu()
-        o_ref, dq_ref, dk_ref, dv_ref, dc_ref = _rows_reference(q, k, v, coef[h].cpu(), rr, d_r)
+        o_ref, dq_ref, dk_ref, dv_ref, dc_ref = _rows_reference(q, k, v, coef[h].cpu(), rr, d_r, freqs_c)
         where = f"b={b} h={h}"
         assert rel_err(out[b, rr, h].float().cpu(), o_ref) < tol, "O " + where
         gb = gx[b].float().cpu()
@@ -273,6 +281,22 @@ def test_cfg2_full_shape_sampled_rows():
 def test_ndiff_long_sampled_rows():
     """N=4 at T=8192 (hs=64): the N-term plan over a long ring."""
     _long_case(B=1, H=2, N=4, hs=64, T=8192, pairs=[(0, 0), (0, 1)], n_rows=32, seed=5)
+
+
+@pytest.mark.parametrize("N", [3, 4])
+def test_cfg3_shape_rope_sampled_rows(N):
+    """BASELINE configs[2]'s attention shape (hs=64, T=2048, H=6, bf16) with RoPE on, as
+    the N-diff model always runs it: the forward rotation pass and the inverse rotation
+    in the dQ / dK epilogues over a ring that wraps T/64 times; N=3 takes the full-dv
+    forward plan, N=4 the dv-chunked one.  O, dQ, dK, dV and d(coef) on sampled rows of
+    (b, h) pairs spread over B=2 x H=6 against fp64."""
+    pairs = [(0, 0), (1, 5), (0, 3), (1, 2)]
+    _long_case(B=2, H=6, N=N, hs=64, T=2048, pairs=pairs, n_rows=40, seed=30 + N, rope=True)
+
+
+def test_cfg2_shape_rope_sampled_rows():
+    """N=2 hs=64 at T=4096 with RoPE (the control-model / rotated path at the cfg2 shape)."""
+    _long_case(B=1, H=4, N=2, hs=64, T=4096, pairs=[(0, 0), (0, 3)], n_rows=32, seed=41, rope=True)
 
 
 def test_backward_reductions_are_reproducible():
