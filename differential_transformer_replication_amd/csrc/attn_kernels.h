@@ -34,62 +34,6 @@
 
 #include <utility>
 
-// dQ kernel: issue every operand read of a branch's S^T ahead of its MFMA chain
-// (1; measured 1% slower at cfg2) or interleave reads with the chain (0, default)
-#ifndef DTA_DQ_AHEAD
-#define DTA_DQ_AHEAD 0
-#endif
-// dK/dV kernel: per-lane DMA source offsets computed once instead of per query tile
-// Measured-and-rejected schedule switches (cfg2 bf16, one-process A/B, tools/ab_kernels.py;
-// medians base -> variant, DESIGN.md "Experiments"):
-//   DTA_DKDV_STAGGER  waves 4-7 defer their dV product by one step   dK/dV 1.547 -> 1.747 ms (8 VGPR spill)
-//   DTA_FWD_LATE / DTA_DKDV_LATE   next tile's DMA after the compute  fwd 1.038 -> 1.035, dK/dV 1.564 -> 1.554 (noise)
-//   DTA_FWD_SPLIT / DTA_DKDV_SPLIT DMA slots spread over the step     fwd 1.010 -> 1.048, dK/dV 1.541 -> 1.616
-#ifndef DTA_DKDV_BQ   // 64: cfg2 8-wave dK/dV 1.543 -> 1.455 ms; superseded by the paired plan (bf16), spills fp16
-#define DTA_DKDV_BQ 32
-#endif
-#ifndef DTA_FWD_LBASE    // forward: per-lane LDS read bases kept in registers across the loop
-#define DTA_FWD_LBASE 1
-#endif
-#ifndef DTA_DQ_LBASE     // dQ: per-lane LDS read bases kept in registers across the loop
-#define DTA_DQ_LBASE 1   // with the DMA offsets precomputed and XA addressing: dQ 1.020 -> 0.994 ms
-#endif
-#ifndef DTA_DKDV_LBASE   // dK/dV: per-lane LDS read bases kept in registers across the loop
-#define DTA_DKDV_LBASE 1
-#endif
-#ifndef DTA_DKDV_STAGGER
-#define DTA_DKDV_STAGGER 0
-#endif
-#ifndef DTA_FWD_LATE
-#define DTA_FWD_LATE 0
-#endif
-#ifndef DTA_DKDV_LATE
-#define DTA_DKDV_LATE 0
-#endif
-#ifndef DTA_FWD_SPLIT
-#define DTA_FWD_SPLIT 0
-#endif
-#ifndef DTA_DKDV_SPLIT
-#define DTA_DKDV_SPLIT 0
-#endif
-#ifndef DTA_FWD_PREOFF   // forward: per-lane K/V DMA source offsets in VGPRs, computed once
-#define DTA_FWD_PREOFF 1
-#endif
-#ifndef DTA_DQ_PREOFF    // dQ: the same
-#define DTA_DQ_PREOFF 1
-#endif
-#ifndef DTA_DKDV_PREOFF
-#define DTA_DKDV_PREOFF 1
-#endif
-// forward: the two waves of a SIMD run half a tile apart (see attn_fwd_kernel)
-#ifndef DTA_FWD_PINGPONG
-#define DTA_FWD_PINGPONG 0
-#endif
-// forward: every branch's QK^T chain before the softmax VALU, one rescale decision per tile
-#ifndef DTA_FWD_QKFIRST
-#define DTA_FWD_QKFIRST 0
-#endif
-
 #ifndef DTA_STAMPS
 #define DTA_STAMPS 0
 #endif
@@ -436,8 +380,7 @@ struct KvRing {
     const int r = pb / VI::ROWB, c = ((pb % VI::ROWB) >> 4) ^ swz<VI::ROWB>(r);
     return (uint32_t)(r * (uint32_t)(st * ES) + c * 16);
   }
-  // slots [UA, UB) of this wave's pieces (the whole tile by default)
-  template <int UA = 0, int UB = MYP>
+  // this wave's pieces of one tile, source offsets computed per tile
   __device__ static void issue(const E* gk, int64_t kst, int64_t ksi, const E* gv, int64_t vst, int k0, int T,
                                E* kdst, E* vdst, int wave, int lane) {
     const int rows = max(0, T - k0);           // a tile past T reads (as zeros) nothing
@@ -446,8 +389,8 @@ struct KvRing {
     const uint32_t nk = (uint32_t)rows * (uint32_t)(kst * ES), nv = (uint32_t)rows * (uint32_t)(vst * ES);
     char* kd = reinterpret_cast<char*>(kdst);
     char* vd = reinterpret_cast<char*>(vdst);
-    sfor<(UB > UA ? UB - UA : 0)>([&](auto U) {
-      constexpr int u = UA + decltype(U)::value;
+    sfor<MYP>([&](auto U) {
+      constexpr int u = decltype(U)::value;
       const int j = u * NW + wave;
       if constexpr ((u + 1) * NW <= PK) {
         buf_lds16(bk, nk, kd + j * 1024, offk(kst, ksi, j, lane));
@@ -504,23 +447,11 @@ inline bool kv_layout_ok(const P& p, int es) {
 }
 
 // ---------------------------------------------------------------- forward ---
-// Paired workgroups (DTA_*_PAIR): 4-wave workgroups sized to 80 KB of LDS, two per
-// CU, so the two waves sharing a SIMD belong to different workgroups (different
-// barriers) instead of one 8-wave workgroup whose SIMD partners run in lockstep
-// (MI355X_MICROARCH.md, two waves per SIMD).  The forward and dQ plans then take
-// 32-key tiles (Q stays in LDS: 32 KB + 3 x 16 KB).
-#ifndef DTA_DKDV_PAIR          // 1: cfg2 dK/dV 1.499 -> 1.406 ms (one-process A/B); fwd / dQ: slower, off
-#define DTA_DKDV_PAIR 1
-#endif
-#ifndef DTA_FWD_PAIR   // 2: fwd 1.004 -> 0.978 ms (branch 0's Q in registers, 64-key tiles); 1 (32-key tiles): slower
-#define DTA_FWD_PAIR 2
-#endif
-#ifndef DTA_FWD_PAIR_AHEAD     // paired forward: S operand reads ahead of the chain (costs registers)
-#define DTA_FWD_PAIR_AHEAD 0
-#endif
-#ifndef DTA_DQ_PAIR    // 2: dQ 1.115 -> 1.013 ms (same plan); 1 (32-key tiles): slower
-#define DTA_DQ_PAIR 2
-#endif
+// Paired workgroups: 4-wave workgroups sized to 80 KB of LDS, two per CU, so the two
+// waves sharing a SIMD belong to different workgroups (different barriers) instead of
+// one 8-wave workgroup whose SIMD partners run in lockstep (MI355X_MICROARCH.md, two
+// waves per SIMD).  cfg2: dK/dV 1.499 -> 1.406 ms; forward / dQ with branch 0's Q rows
+// in registers and 64-key tiles: fwd 1.004 -> 0.978, dQ 1.115 -> 1.013 ms.
 constexpr int ring_stages_lim(int fixed_bytes, int tile_bytes, int lim) {
   return (fixed_bytes + 4 * tile_bytes <= lim) ? 4 : (fixed_bytes + 3 * tile_bytes <= lim) ? 3 : 2;
 }
@@ -529,22 +460,21 @@ template <class E> struct FwdTile { static constexpr int BN = 64; };
 template <> struct FwdTile<float> { static constexpr int BN = 32; };
 
 // dv chunk per forward workgroup: keep N * DVC/2 accumulator VGPRs <= 128
-#ifndef DTA_FWD_FULLDV   // N * dv / 2 <= this many accumulator VGPRs: one workgroup takes the whole dv
-#define DTA_FWD_FULLDV 192
-#endif
+// N * dv / 2 <= this many accumulator VGPRs: one workgroup takes the whole dv
+constexpr int kFwdFullDv = 192;
 template <int N, int DV, bool B16 = true>
 struct FwdChunk {
   // 16-bit: N = 3 at dv = 128 takes the whole dv in one (one-wave-per-SIMD) workgroup
   // instead of two dv chunks that each redo QK^T and the softmax (fwd 0.523 -> 0.470 ms
   // at cfg3's shape); N = 4 spills that way
-  static constexpr int cap = (B16 && N * DV / 2 <= DTA_FWD_FULLDV) ? DV : (256 / N) / 32 * 32;
+  static constexpr int cap = (B16 && N * DV / 2 <= kFwdFullDv) ? DV : (256 / N) / 32 * 32;
   static constexpr int DVC = DV <= cap ? DV : (cap >= 128 && DV % 128 == 0 ? 128 : (cap >= 64 ? 64 : 32));
 };
 
 template <class E, int HS, int N, int DVC, int NW, bool QREG, int QRH = 0>
 struct FwdCfg {
   // QRH > 0 (paired plan): the first QRH branches' Q rows stay in registers
-  static constexpr bool PAIR = DTA_FWD_PAIR && NW == 4 && !QREG && sizeof(E) == 2 && N * DVC / 2 <= 128;
+  static constexpr bool PAIR = NW == 4 && !QREG && sizeof(E) == 2 && N * DVC / 2 <= 128;
   static constexpr int BN = (PAIR && QRH == 0) ? 32 : FwdTile<E>::BN;
   static constexpr int BM = NW * 32;
   static constexpr int nQ = QREG ? 0 : (N - QRH) * BM * HS;
@@ -570,10 +500,10 @@ struct FwdPick {
   static constexpr bool q8 = NWMAX >= 8 && FwdCfg<E, HS, N, DVC, 8, false>::bytes <= LIM &&
                              FwdCfg<E, HS, N, DVC, 8, false>::regs <= 280;
   static constexpr bool q4 = FwdCfg<E, HS, N, DVC, 4, false>::bytes <= LIM;
-  // DTA_FWD_PAIR = 2: paired 4-wave plan with 64-key tiles and branch 0's Q in registers
-  static constexpr int QRH = (DTA_FWD_PAIR == 2 && q8 && N >= 2 &&
+  // paired 4-wave plan with 64-key tiles and branch 0's Q in registers
+  static constexpr int QRH = (q8 && N >= 2 &&
                               FwdCfg<E, HS, N, DVC, 4, false, 1>::bytes <= 80 * 1024) ? 1 : 0;
-  static constexpr bool pair = !NP && DTA_FWD_PAIR && (DTA_FWD_PAIR == 1 || QRH == 1) && q8 &&
+  static constexpr bool pair = !NP && QRH == 1 && q8 &&
                                 FwdCfg<E, HS, N, DVC, 4, false, QRH>::PAIR &&
                                 FwdCfg<E, HS, N, DVC, 4, false, QRH>::bytes <= 80 * 1024;
   static constexpr int QH = pair ? QRH : 0;
@@ -644,16 +574,15 @@ void attn_fwd_kernel(FwdParams p) {
   const int kend = min(T, q0 + BM);
   const int ntiles = (kend + BN - 1) / BN;
   using KR = KvRing<E, HS, N, DVC, BN, NW>;
-  // DTA_FWD_PREOFF: this wave's per-lane DMA source offsets computed once (VGPRs)
-  constexpr bool PRE = DTA_FWD_PREOFF && SRD;
+  // this wave's per-lane DMA source offsets computed once (VGPRs): a tile then costs only
+  // its two scalar descriptors and M0 (in-kernel stamps: fwd 0.979 -> 0.901 ms at cfg2)
+  constexpr bool PRE = SRD;
   uint32_t doff[PRE ? KR::MYP : 1];
   if constexpr (PRE) KR::offsets(p.k.st, p.k.si, p.v.st, wave, lane, doff);
   auto stage_kv = [&](int kt, int buf) {
     const int k0 = kt * BN;
     if constexpr (PRE) {
       KR::issue_pre(gk, p.k.st, gv, p.v.st, k0, T, Kb + buf * N * BN * HS, Vb + buf * BN * DVC, wave, doff);
-    } else if constexpr (SRD) {
-      KR::issue(gk, p.k.st, p.k.si, gv, p.v.st, k0, T, Kb + buf * N * BN * HS, Vb + buf * BN * DVC, wave, lane);
     } else {
 #pragma unroll
       for (int i = 0; i < N; ++i)
@@ -663,42 +592,10 @@ void attn_fwd_kernel(FwdParams p) {
   };
   const int tile_pieces = SRD ? KR::pieces(wave)
                               : N * stage_pieces<E, HS, BN, HS, NW>(wave) + stage_pieces<E, DVC, BN, DVC, NW>(wave);
-  // DTA_FWD_SPLIT: a wave's DMA pieces for tile kt+NS-1 go out one slot at a time over
-  // the step (slot 0 after the barrier, slot i+1 after branch i's S chain, the rest
-  // before PV) instead of all at once, so the workgroup's pieces do not queue together
-  constexpr bool FSPLIT = DTA_FWD_SPLIT && SRD && !DTA_FWD_PINGPONG && KR::MYP >= 2;
-  int split_kt = 0;
-  bool split_iss = false;
-  auto issue_slots = [&](auto UA, auto UB) {
-    constexpr int a = decltype(UA)::value < KR::MYP ? decltype(UA)::value : KR::MYP;
-    constexpr int e = decltype(UB)::value < KR::MYP ? decltype(UB)::value : KR::MYP;
-    if constexpr (e > a) {
-      const int kn = split_kt + NS - 1, bn = kn % NS;
-      if (split_iss)
-        KR::template issue<a, e>(gk, p.k.st, p.k.si, gv, p.v.st, kn * BN, T, Kb + bn * N * BN * HS,
-                                 Vb + bn * BN * DVC, wave, lane);
-    }
-  };
-  // Ping-pong (PP): the two waves sharing a SIMD (w and w+4) run half a tile apart --
-  // one in its QK^T + softmax phase (A) while the other is in its PV phase (B) -- so
-  // the VALU-heavy half of one overlaps the MFMA-only half of the other instead of
-  // both hitting the VALU at once (MI355X_MICROARCH.md, two waves per SIMD).  The
-  // second half (G1) passes one extra barrier before the loop, the first half (G0)
-  // one after it.  Ring protocol (NS = 3 stages, checked in DESIGN.md): G0 stages
-  // tile t+1 at the start of its A(t) and waits for it at the end of its B(t); G1
-  // stages tile t+2 at the start of its B(t) and waits for tile t+1 at the end of
-  // its A(t).  Every buffer is refilled only after both halves finished its tile.
-  constexpr bool PP = DTA_FWD_PINGPONG && NW == 8 && SRD && sizeof(E) == 2 && CF::NS == 3;
-  const bool g1 = PP && wave >= NW / 2;
-  if constexpr (PP) {
-    if (ntiles > 0) stage_kv(0, 0);
-    if (g1 && ntiles > 1) stage_kv(1, 1);
-    wait_vm(g1 && ntiles > 1 ? tile_pieces : 0);               // tile 0 (and the Q block) landed
-  } else {
-    for (int j = 0; j < NS - 1; ++j)
-      if (j < ntiles) stage_kv(j, j);
-    wait_vm(tile_pieces * max(0, min(NS - 1, ntiles) - 1));   // tile 0 (and the Q block) landed
-  }  lds_barrier();
+  for (int j = 0; j < NS - 1; ++j)
+    if (j < ntiles) stage_kv(j, j);
+  wait_vm(tile_pieces * max(0, min(NS - 1, ntiles) - 1));   // tile 0 (and the Q block) landed
+  lds_barrier();
 
   f32x16 acc[N][NDB];
   float m[N], l[N];
@@ -710,10 +607,8 @@ void attn_fwd_kernel(FwdParams p) {
     for (int d = 0; d < NDB; ++d) acc[i][d] = f32x16{};
   }
   const bool wave_live = qw0 < T;
-  // static priority for the second-dispatched half (MI355X_MICROARCH.md, two waves per SIMD, item 4)
-  if (NW == 8 && p.prio && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
 
-  // per-lane LDS read bases kept in registers across the loop (DTA_FWD_LBASE; see attn_dkdv_kernel)
+  // per-lane LDS read bases kept in registers across the loop (see attn_dkdv_kernel)
   int LrK = 0, LtV = 0;
   if constexpr (sizeof(E) == 2) { LrK = row_lane<KI::ROWB>(lane); LtV = tr_lane<VI::ROWB>(lane); }
   // key = k0 + kb*32 + rowof(r); masked when key > qrow or key >= T
@@ -803,7 +698,7 @@ void attn_fwd_kernel(FwdParams p) {
         const char* qbase = reinterpret_cast<const char*>(Qs + (i >= NQR ? i - NQR : 0) * BM * HS) + wave * 32 * QI::ROWB;
 #pragma unroll
         for (int kb = 0; kb < NKB; ++kb) sa[i][kb] = f32x16{};
-        if constexpr (NSQ * (NKB + 1) <= 12 && (QRH == 0 || DTA_FWD_PAIR_AHEAD)) {
+        if constexpr (NSQ * (NKB + 1) <= 12 && QRH == 0) {
           // every operand read of this branch's S^T issued ahead of its MFMA chain,
           // so the chain waits on the LDS latency once instead of per k-step
           // (head sizes <= 64; at 128 the 24 fragments do not fit the registers)
@@ -848,37 +743,7 @@ void attn_fwd_kernel(FwdParams p) {
           }
         }
       }
-      if constexpr (FSPLIT) {
-        if (i == 0) issue_slots(std::integral_constant<int, 1>{}, std::integral_constant<int, 2>{});
-        else if (i == 1) issue_slots(std::integral_constant<int, 2>{}, std::integral_constant<int, 3>{});
-        else if (i == 2) issue_slots(std::integral_constant<int, 3>{}, std::integral_constant<int, 4>{});
-      }
-      if constexpr (!DTA_FWD_QKFIRST) softmax_branch(i, k0, MASKED, sa[i], pf[i]);
-    }
-    if constexpr (DTA_FWD_QKFIRST) {
-      // every branch's S^T first (above), then the maxima and ONE rescale decision for all
-      // branches, so the VALU of branch 0 can run beside branch 1's MFMA chain
-      float mx[N];
-      bool grow = false;
-#pragma unroll
-      for (int i = 0; i < N; ++i) {
-        if constexpr (MASK) mask_scores(k0, sa[i]);
-        mx[i] = wave_max_halves(row_max(sa[i])) * p.sl2;
-        grow = grow || mx[i] > m[i] + THR;
-      }
-      if (__any(grow)) {
-#pragma unroll
-        for (int i = 0; i < N; ++i) {
-          const float mnew = fmaxf(m[i], mx[i]);
-          const float alpha = exp2_fast(m[i] - mnew);
-          m[i] = mnew;
-          l[i] *= alpha;
-#pragma unroll
-          for (int d = 0; d < NDB; ++d) acc[i][d] *= alpha;
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < N; ++i) exp_pack(i, k0, sa[i], pf[i]);
+      softmax_branch(i, k0, MASKED, sa[i], pf[i]);
     }
   };
   // O_i^T += V^T P_i^T, one V fragment feeds every branch
@@ -924,367 +789,34 @@ void attn_fwd_kernel(FwdParams p) {
     // keep lane-derived addresses loop-variant: recomputed per tile instead of
     // hoisted into (spilled) registers across the whole loop
     asm volatile("" : "+v"(lane));
-    if constexpr (DTA_FWD_LBASE && sizeof(E) == 2) {
-      asm volatile("" : "+v"(LrK), "+v"(LtV));
-    } else if constexpr (sizeof(E) == 2) {
-      LrK = row_lane<KI::ROWB>(lane); LtV = tr_lane<VI::ROWB>(lane);
-    }
+    if constexpr (sizeof(E) == 2) asm volatile("" : "+v"(LrK), "+v"(LtV));
     tid = (wave << 6) + lane; hf = lane >> 5; c32 = lane & 31;
     qrow = qw0 + c32;
     const bool live = wave_live && kt * BN <= qw0 + 31;
     st.lap<7>();
-    if constexpr (PP) {
-      if (!g1 && kt + 1 < ntiles) stage_kv(kt + 1, (kt + 1) % NS);
-      frag pf[N][NKB * SPB];
-      if (live) phase_a(kt, MASKED, pf);
-      if (g1) wait_vm(0);                    // tile kt+1 (staged at B(kt-1)) before G0 reads it
-      lds_barrier();
-      if (g1 && kt + 2 < ntiles) stage_kv(kt + 2, (kt + 2) % NS);
-      if (live) phase_b(kt, pf);
-      if (!g1) wait_vm(0);                   // tile kt+1 (staged at A(kt))
-      lds_barrier();
-    } else {
-      if constexpr (FSPLIT) {
-        split_kt = kt;
-        split_iss = kt + NS - 1 < ntiles;
-        issue_slots(std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{});
-        if (!live) issue_slots(std::integral_constant<int, 1>{}, std::integral_constant<int, KR::MYP>{});
-      } else if (!DTA_FWD_LATE && kt + NS - 1 < ntiles) {
-        stage_kv(kt + NS - 1, (kt + NS - 1) % NS);
-      }
-      st.lap<0>();
-      if (live) {
-        frag pf[N][NKB * SPB];
-        phase_a(kt, MASKED, pf);
-        if constexpr (FSPLIT) issue_slots(std::integral_constant<int, (N < 3 ? N : 3) + 1>{},
-                                          std::integral_constant<int, KR::MYP>{});
-        st.lap<1>();
-        phase_b(kt, pf);
-        st.lap<2>();
-      }
-      // DTA_FWD_LATE: the next tile's DMA goes out after the compute, beside the barrier wait
-      if constexpr (DTA_FWD_LATE && !FSPLIT) if (kt + NS - 1 < ntiles) stage_kv(kt + NS - 1, (kt + NS - 1) % NS);
-      // tile kt+1 must have landed; younger tiles may stay in flight
-      wait_vm(tile_pieces * max(0, min(NS - 2, ntiles - 2 - kt)));
-      st.lap<3>();
-      lds_barrier();
-      st.lap<4>();
-    }
-  };
-  st.start();
-  if (g1) lds_barrier();                     // PP: the second half starts one phase behind
-  const int nfull = min(ntiles, min((q0 + 1) / BN, T / BN));
-  for (int kt = 0; kt < nfull; ++kt) step(kt, std::false_type{});
-  for (int kt = nfull; kt < ntiles; ++kt) step(kt, std::true_type{});
-  if (PP && !g1) lds_barrier();              // ... and the first half ends one phase later
-  st.lap<5>();
-  st.flush(p.stamps, lin * NW + wave, lane);
-
-  if (!wave_live || qrow >= T) return;
-  float inv[N];
-#pragma unroll
-  for (int i = 0; i < N; ++i) {
-    const float lt = wave_sum_halves(l[i]);
-    inv[i] = 1.f / lt;
-    if (dc0 == 0 && hf == 0)
-      p.lse[(((int64_t)i * p.B + b) * p.H + hh) * T + qrow] = -(m[i] + __builtin_log2f(lt));   // stored negated
-  }
-  E* go = reinterpret_cast<E*>(p.o.p) + b * p.o.sb + (int64_t)qrow * p.o.st + hh * p.o.sh + dc0;
-  E* gob = reinterpret_cast<E*>(p.obr.p) + b * p.obr.sb + (int64_t)qrow * p.obr.st + hh * p.obr.sh + dc0;
-#pragma unroll
-  for (int d = 0; d < NDB; ++d)
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int e = d * 32 + 8 * g + 4 * hf;
-      float o0 = 0.f, o1 = 0.f, o2 = 0.f, o3 = 0.f;
-#pragma unroll
-      for (int i = 0; i < N; ++i) {
-        const float a0 = acc[i][d][4 * g + 0] * inv[i], a1 = acc[i][d][4 * g + 1] * inv[i];
-        const float a2 = acc[i][d][4 * g + 2] * inv[i], a3 = acc[i][d][4 * g + 3] * inv[i];
-        store4<E>(gob + i * p.obr.si + e, a0, a1, a2, a3);
-        o0 = fmaf(coef[i], a0, o0); o1 = fmaf(coef[i], a1, o1);
-        o2 = fmaf(coef[i], a2, o2); o3 = fmaf(coef[i], a3, o3);
-      }
-      store4<E>(go + e, o0, o1, o2, o3);
-    }
-}
-
-// --------------------------------------- forward, software-pipelined ---
-//
-// One wave per SIMD (4 waves x 32 query rows; the whole 512-entry register file),
-// Q fragments in registers, K/V tiles through a 4-stage LDS-DMA ring.  The loop
-// body is straight-line: after this tile's maxima (and the rare rescale), it
-// issues the NEXT tile's QK^T MFMAs, this tile's exp / row sums / P packing and
-// this tile's PV MFMAs in one basic block, so one wave keeps its MFMA pipe fed
-// while its own softmax VALU runs -- instead of relying on two lockstepped waves
-// per SIMD, whose VALU phases coincide at every tile barrier (measured: 36% of the
-// forward's cycles in one shared phase, tools/stamps.py).
-// Ring: tile t+3 is staged (unconditionally: past T it reads nothing) at the top of
-// iteration t into the buffer of tile t-1, whose V was last read before the barrier
-// that ended iteration t-1 and whose K before the one that ended t-2; iteration t
-// ends with tile t+2 landed (K(t+2) feeds the next iteration's QK^T).
-#ifndef DTA_FWD_PIPE_BN
-#define DTA_FWD_PIPE_BN 32   // 64: 1.088-1.133 ms, 32: 1.195 ms vs 1.02 for the 8-wave kernel (cfg2 A/B)
-#endif
-#ifndef DTA_FWD_PIPE_SGB      // 5: 1.230 ms, 8: 1.225 ms vs 1.124 (pipe, BN 64) and 1.017 (8-wave kernel)
-#define DTA_FWD_PIPE_SGB 0
-#endif
-#ifndef DTA_FWD_PIPE_PINQ
-#define DTA_FWD_PIPE_PINQ 0
-#endif
-template <class E, int HS, int N, int DVC>
-struct FwdPipeCfg {
-  static constexpr int NW = 4, BM = NW * 32, BN = DTA_FWD_PIPE_BN, NKB = BN / 32;
-  static constexpr int nK = N * BN * HS, nV = BN * DVC;
-  static constexpr int NS = 4;
-  static constexpr int bytes = NS * (nK + nV) * (int)sizeof(E);
-  // O accumulators, two score tiles, Q fragments, P, K operand reads, misc
-  static constexpr int regs = N * DVC / 2 + 2 * N * NKB * 16 + N * HS / 4 + N * NKB * 8 + NKB * HS / 2 + 64;
-  static constexpr bool ok = sizeof(E) == 2 && HS >= 32 && bytes <= 160 * 1024 && regs <= 480 &&
-                             KvRing<E, HS, N, DVC, BN, NW>::ok;
-};
-
-template <class E, int HS, int N, int DVC>
-__global__ __launch_bounds__(256, 1) void attn_fwd_pipe_kernel(FwdParams p) {
-  using O = Ops<E>;
-  using frag = typename O::frag;
-  using KI = Img<E, HS>;
-  using VI = Img<E, DVC>;
-  using CF = FwdPipeCfg<E, HS, N, DVC>;
-  constexpr int NW = CF::NW, BN = CF::BN, BM = CF::BM, NS = CF::NS;
-  constexpr int KS = O::KSTEP, NSQ = HS / KS, NKB = CF::NKB, NDB = DVC / 32;
-  constexpr float THR = 8.f;        // deferred-rescale threshold (log2 units): P <= 2^8
-
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  E* Kb = reinterpret_cast<E*>(smem);     // [NS][N][BN][HS]
-  E* Vb = Kb + NS * CF::nK;               // [NS][BN][DVC]
-
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63, hf = lane >> 5, c32 = lane & 31;
-  const int nblk = gridDim.x * gridDim.y * gridDim.z;
-  const int lin = xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z), nblk);
-  const int bx = lin % gridDim.x, by = (lin / gridDim.x) % gridDim.y, bz = lin / (gridDim.x * gridDim.y);
-  const int nch = p.DV / DVC;
-  const int qt = gridDim.x - 1 - bx;                   // longest causal rows first
-  const int hh = by / nch, dc0 = (by % nch) * DVC;
-  const int b = bz;
-  const int T = p.T;
-  const int q0 = qt * BM, qw0 = q0 + wave * 32;
-  const int qrow = qw0 + c32;
-
-  const E* gq = reinterpret_cast<const E*>(p.q.p) + b * p.q.sb + hh * p.q.sh;
-  const E* gk = reinterpret_cast<const E*>(p.k.p) + b * p.k.sb + hh * p.k.sh;
-  const E* gv = reinterpret_cast<const E*>(p.v.p) + b * p.v.sb + hh * p.v.sh + dc0;
-  float coef[N];
-#pragma unroll
-  for (int i = 0; i < N; ++i) coef[i] = p.coef[hh * N + i];
-
-  // this wave's query rows as B fragments of S^T = K Q^T (rows past T read as zeros)
-  frag qf[N][NSQ];
-#pragma unroll
-  for (int i = 0; i < N; ++i)
-#pragma unroll
-    for (int s = 0; s < NSQ; ++s)
-      qf[i][s] = qrow < T ? O::load_global(gq + (int64_t)qrow * p.q.st + i * p.q.si + s * KS + hf * O::KH) : O::zero();
-
-  const int kend = min(T, q0 + BM);
-  const int ntiles = (kend + BN - 1) / BN;
-  using KR = KvRing<E, HS, N, DVC, BN, NW>;
-  const int pieces = KR::pieces(wave);
-  uint32_t doff[KR::MYP];
-  KR::offsets(p.k.st, p.k.si, p.v.st, wave, lane, doff);
-  auto stage_kv = [&](int kt) {
-    const int buf = kt % NS;
-    KR::issue_pre(gk, p.k.st, gv, p.v.st, kt * BN, T, Kb + buf * N * BN * HS, Vb + buf * BN * DVC, wave, doff);
-  };
-#pragma unroll
-  for (int j = 0; j < NS - 1; ++j) stage_kv(j);
-  wait_vm(pieces);                       // tiles 0 and 1 landed (tile 2 may fly)
-  lds_barrier();
-
-  f32x16 acc[N][NDB];
-  float m[N], l[N];
-#pragma unroll
-  for (int i = 0; i < N; ++i) {
-    m[i] = -INFINITY;
-    l[i] = 0.f;
-#pragma unroll
-    for (int d = 0; d < NDB; ++d) acc[i][d] = f32x16{};
-  }
-  // O accumulators and Q fragments are MFMA operands only: keep them in AGPRs, the
-  // VGPRs for the two score tiles the softmax VALU works on
-  auto pin = [&]() {
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-#pragma unroll
-      for (int d = 0; d < NDB; ++d) asm volatile("" : "+a"(acc[i][d]));
-      if constexpr (DTA_FWD_PIPE_PINQ) {
-#pragma unroll
-        for (int s = 0; s < NSQ; ++s) asm volatile("" : "+a"(qf[i][s]));
-      }
-    }
-  };
-  pin();
-
-  // S^T of tile kt for every branch (all operand reads ahead of each branch's chain)
-  auto qk = [&](int kt, f32x16 (&sc)[N][NKB]) {
-    const char* kbase = reinterpret_cast<const char*>(Kb + (kt % NS) * N * BN * HS);
-    const int Lr = row_lane<KI::ROWB>(lane);
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-      frag kfr[NKB][NSQ];
-#pragma unroll
-      for (int s = 0; s < NSQ; ++s)
-#pragma unroll
-        for (int kb = 0; kb < NKB; ++kb)
-          kfr[kb][s] = *reinterpret_cast<const frag*>(kbase + (i * BN + kb * 32) * KI::ROWB + (Lr ^ (32 * s)));
-#pragma unroll
-      for (int kb = 0; kb < NKB; ++kb) sc[i][kb] = f32x16{};
-#pragma unroll
-      for (int s = 0; s < NSQ; ++s)
-#pragma unroll
-        for (int kb = 0; kb < NKB; ++kb) sc[i][kb] = O::mma(kfr[kb][s], qf[i][s], sc[i][kb]);
-    }
-  };
-
-  f32x16 sa[N][NKB], sb[N][NKB];
-  float mx[N];                           // scale*log2e * row max of the pending tile's scores, per branch
-  // mask (diagonal / past-T tiles) and row maxima of tile kt's raw scores
-  auto mask_max = [&](int kt, auto MASKED, f32x16 (&sc)[N][NKB]) {
-    const int k0 = kt * BN;
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-      if constexpr (decltype(MASKED)::value) {
-        const int lim = min(qrow, T - 1) - k0 - 4 * hf;     // key > qrow or key >= T: masked
-#pragma unroll
-        for (int kb = 0; kb < NKB; ++kb)
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            sc[i][kb][r] = (kb * 32 + (r & 3) + 8 * (r >> 2) > lim) ? -INFINITY : sc[i][kb][r];
-      }
-      float a = -INFINITY, c = -INFINITY;
-#pragma unroll
-      for (int kb = 0; kb < NKB; ++kb)
-#pragma unroll
-        for (int r = 0; r < 16; r += 4) {
-          a = fmaxf(fmaxf(a, sc[i][kb][r]), sc[i][kb][r + 1]);
-          c = fmaxf(fmaxf(c, sc[i][kb][r + 2]), sc[i][kb][r + 3]);
-        }
-      mx[i] = wave_max_halves(fmaxf(a, c)) * p.sl2;
-    }
-  };
-  const int nunm = min(ntiles, min((q0 + 1) / BN, T / BN));       // tiles that need no mask
-  qk(0, sa);
-  if (nunm > 0) mask_max(0, std::false_type{}, sa);
-  else mask_max(0, std::true_type{}, sa);
-
-  Stamps st;
-  // iteration kt: rescale decision for tile kt (maxima from the previous block), then ONE
-  // straight-line block: stage tile kt+3, QK^T of tile kt+1, exp / pack / PV of tile kt,
-  // then mask + maxima of tile kt+1 (its MFMAs have drained behind this tile's PV)
-  auto iter = [&](int kt, auto MASKNEXT, auto NEXT, f32x16 (&sc)[N][NKB], f32x16 (&sn)[N][NKB]) {
-    constexpr bool HAS_NEXT = decltype(NEXT)::value;
-    bool grow = false;
-#pragma unroll
-    for (int i = 0; i < N; ++i) grow = grow || mx[i] > m[i] + THR;
-    if (__any(grow)) {
-      asm volatile("" ::: "memory");     // a real (rare) branch, never speculated into every tile
-#pragma unroll
-      for (int i = 0; i < N; ++i) {
-        const float mnew = fmaxf(m[i], mx[i]);
-        const float alpha = exp2_fast(m[i] - mnew);
-        m[i] = mnew;
-        l[i] *= alpha;
-#pragma unroll
-        for (int d = 0; d < NDB; ++d) acc[i][d] *= alpha;
-      }
-    }
+    if (kt + NS - 1 < ntiles) stage_kv(kt + NS - 1, (kt + NS - 1) % NS);
     st.lap<0>();
-    stage_kv(kt + NS - 1);
-    st.lap<1>();
-    if constexpr (HAS_NEXT) qk(kt + 1, sn);
-    frag pf[N][NKB * 2];
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-      const float mi = m[i];
-      float s0 = 0.f, s1 = 0.f;
-#pragma unroll
-      for (int kb = 0; kb < NKB; ++kb) {
-#pragma unroll
-        for (int r = 0; r < 16; r += 2) {
-          const float e0 = exp2_fast(fmaf(sc[i][kb][r], p.sl2, -mi));
-          const float e1 = exp2_fast(fmaf(sc[i][kb][r + 1], p.sl2, -mi));
-          sc[i][kb][r] = e0;
-          sc[i][kb][r + 1] = e1;
-          s0 += e0;
-          s1 += e1;
-        }
-        pf[i][kb * 2 + 0] = O::template pack<0>(sc[i][kb]);
-        pf[i][kb * 2 + 1] = O::template pack<1>(sc[i][kb]);
-      }
-      l[i] += s0 + s1;
+    if (live) {
+      frag pf[N][NKB * SPB];
+      phase_a(kt, MASKED, pf);
+      st.lap<1>();
+      phase_b(kt, pf);
+      st.lap<2>();
     }
-    {
-      const unsigned vb = lds_addr(Vb + (kt % NS) * BN * DVC);
-      const int Lv = tr_lane<VI::ROWB>(lane);
-      sfor<NDB>([&](auto D) {
-        constexpr int d = decltype(D)::value;
-        lds64 r[NKB][4];
-        const unsigned a0 = vb + (Lv ^ (64 * d)), a1 = vb + (Lv ^ (64 * d + 32));
-        sfor<NKB>([&](auto KB) { tr_issue<VI::ROWB, 32 * decltype(KB)::value>(r[decltype(KB)::value], a0, a1); });
-        lgkm_pin<NKB>(r);
-#pragma unroll
-        for (int kb = 0; kb < NKB; ++kb)
-#pragma unroll
-          for (int s = 0; s < 2; ++s) {
-            const frag va = tr_frag<E>(r[kb], s);
-#pragma unroll
-            for (int i = 0; i < N; ++i) acc[i][d] = O::mma(va, pf[i][kb * 2 + s], acc[i][d]);
-          }
-      });
-    }
-    if constexpr (HAS_NEXT) mask_max(kt + 1, MASKNEXT, sn);
-    // DTA_FWD_PIPE_SGB = v: ask the scheduler for one MFMA then up to v VALU, throughout
-    // the block (LDS reads two per group up front), instead of its own clustering
-    if constexpr (DTA_FWD_PIPE_SGB > 0) {
-      constexpr int MF = (HAS_NEXT ? N * NKB * NSQ : 0) + NDB * NKB * 2 * N;
-      sfor<MF>([&](auto) {
-        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, DTA_FWD_PIPE_SGB, 0);
-      });
-    }
-    pin();
-    st.lap<2>();
-    wait_vm(pieces);                     // tile kt+2 landed; tile kt+3 may fly
+    // tile kt+1 must have landed; younger tiles may stay in flight
+    wait_vm(tile_pieces * max(0, min(NS - 2, ntiles - 2 - kt)));
     st.lap<3>();
     lds_barrier();
     st.lap<4>();
   };
-  auto copy_scores = [&]() {
-#pragma unroll
-    for (int i = 0; i < N; ++i)
-#pragma unroll
-      for (int kb = 0; kb < NKB; ++kb) sa[i][kb] = sb[i][kb];
-  };
-  const std::true_type Y{};
-  const std::false_type F{};
-  // iterations whose NEXT tile needs no mask: kt + 1 < nunm
-  const int n1 = max(0, min(ntiles - 1, nunm - 1));
-  int kt = 0;
   st.start();
-  // two at a time, the score tiles alternating (no register copies)
-  for (; kt + 2 <= n1; kt += 2) {
-    iter(kt, F, Y, sa, sb);
-    iter(kt + 1, F, Y, sb, sa);
-  }
-  for (; kt < n1; ++kt) { iter(kt, F, Y, sa, sb); copy_scores(); }
-  for (; kt < ntiles - 1; ++kt) { iter(kt, Y, Y, sa, sb); copy_scores(); }
-  if (ntiles > 0) iter(ntiles - 1, Y, F, sa, sb);
-  wait_vm(0);                            // no LDS-DMA left in flight at exit
+  const int nfull = min(ntiles, min((q0 + 1) / BN, T / BN));
+  for (int kt = 0; kt < nfull; ++kt) step(kt, std::false_type{});
+  for (int kt = nfull; kt < ntiles; ++kt) step(kt, std::true_type{});
+  st.lap<5>();
   st.flush(p.stamps, lin * NW + wave, lane);
 
-  if (qw0 >= T || qrow >= T) return;
+  if (!wave_live || qrow >= T) return;
   float inv[N];
 #pragma unroll
   for (int i = 0; i < N; ++i) {
@@ -1318,7 +850,7 @@ template <class E, int HS, int N, int DV, int NW, bool QREG, int QRH = 0>
 struct DqCfg {
   // QRH > 0 (paired plan): the first QRH branches' Q rows stay in registers, the
   // rest in LDS, so Q plus a 2-stage ring of 64-key tiles fits 80 KB
-  static constexpr bool PAIR = DTA_DQ_PAIR && NW == 4 && !QREG && sizeof(E) == 2;
+  static constexpr bool PAIR = NW == 4 && !QREG && sizeof(E) == 2;
   static constexpr int BN = (PAIR && QRH == 0) ? 32 : FwdTile<E>::BN;
   static constexpr int BM = NW * 32;
   static constexpr int HSP = HS < 32 ? 32 : HS;
@@ -1334,11 +866,11 @@ template <class E, int HS, int N, int DV = 2 * HS, bool NP = false>
 struct DqPick {
   static constexpr int LIM = 160 * 1024;
   static constexpr bool q8 = sizeof(E) == 2 && DqCfg<E, HS, N, DV, 8, false>::bytes <= LIM;
-  // DTA_DQ_PAIR = 2: paired 4-wave plan with 64-key tiles and branch 0's Q in registers
-  static constexpr int QRH = (DTA_DQ_PAIR == 2 && q8 && N >= 2 &&
+  // paired 4-wave plan with 64-key tiles and branch 0's Q in registers
+  static constexpr int QRH = (q8 && N >= 2 &&
                               DqCfg<E, HS, N, DV, 4, false, 1>::bytes <= 80 * 1024) ? 1 : 0;
   // (head size >= 64: the hs = 32, N = 3 paired plan spills)
-  static constexpr bool pair = !NP && DTA_DQ_PAIR && (DTA_DQ_PAIR == 1 || QRH == 1) && q8 && HS >= 64 &&
+  static constexpr bool pair = !NP && QRH == 1 && q8 && HS >= 64 &&
                                DqCfg<E, HS, N, DV, 4, false, QRH>::bytes <= 80 * 1024;
   static constexpr int NW = pair ? 4 : (q8 ? 8 : (sizeof(E) == 2 ? 4 : 2));
   static constexpr bool QREG = pair ? false : !q8;
@@ -1393,7 +925,7 @@ void attn_dq_kernel(BwdParams p) {
   const int ntiles = (kend + BN - 1) / BN;
   using KR = KvRing<E, HS, N, DV, BN, NW>;
   static_assert(!SRD || HSP == HS, "descriptor staging needs unpadded K rows");
-  constexpr bool PRE = DTA_DQ_PREOFF && SRD && !DROP;  // DMA source offsets computed once (dropout: fewer spills without)
+  constexpr bool PRE = SRD && !DROP;  // DMA source offsets computed once (dropout: fewer spills without)
   uint32_t doff[PRE ? KR::MYP : 1];
   if constexpr (PRE) KR::offsets(p.k.st, p.k.si, p.v.st, wave, lane, doff);
   auto stage_kv = [&](int kt, int buf) {
@@ -1478,16 +1010,15 @@ void attn_dq_kernel(BwdParams p) {
 #pragma unroll
     for (int d = 0; d < NHB; ++d) dq[i][d] = f32x16{};
   const bool wave_live = qw0 < T;
-  // static priority for the second-dispatched half (MI355X_MICROARCH.md, two waves per SIMD, item 4)
-  if (NW == 8 && p.prio && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
 
   // unmasked loop, then the block's diagonal / tail tiles (see attn_fwd_kernel)
-  // per-lane LDS read bases kept in registers across the loop (DTA_DQ_LBASE; see attn_dkdv_kernel)
+  // per-lane LDS read bases kept in registers across the loop (see attn_dkdv_kernel);
+  // with dropout they are re-derived per step (fewer spills)
   int LrV = 0, LrK = 0, LrQ = 0, LtK = 0;
   // XA (see attn_dkdv_kernel): the ring slot's base added once per step, the k-step XOR after it
   constexpr int XMAX = 32 * ((NSV > NSQ ? NSV : NSQ) - 1) + 64 * (NHB - 1) + 32;
   constexpr int XM = XMAX < 256 ? 256 : (XMAX < 512 ? 512 : 1024);
-  constexpr bool XA = DTA_DQ_LBASE && !DROP && SRD && sizeof(E) == 2 && (CF::nQ * (int)sizeof(E)) % XM == 0 &&
+  constexpr bool XA = !DROP && SRD && sizeof(E) == 2 && (CF::nQ * (int)sizeof(E)) % XM == 0 &&
                       (CF::nK * (int)sizeof(E)) % XM == 0 && (CF::nV * (int)sizeof(E)) % XM == 0;
   if constexpr (sizeof(E) == 2) {
     LrV = row_lane<VI::ROWB>(lane); LrK = row_lane<KI::ROWB>(lane); LrQ = row_lane<QI::ROWB>(lane);
@@ -1498,7 +1029,7 @@ void attn_dq_kernel(BwdParams p) {
     // keep lane-derived addresses loop-variant: recomputed per tile instead of
     // hoisted into (spilled) registers across the whole loop
     asm volatile("" : "+v"(lane));
-    if constexpr (DTA_DQ_LBASE && !DROP && sizeof(E) == 2) {
+    if constexpr (!DROP && sizeof(E) == 2) {
       asm volatile("" : "+v"(LrV), "+v"(LrK), "+v"(LtK));
       if constexpr (QI::ROWB == KI::ROWB) LrQ = LrK;
       else asm volatile("" : "+v"(LrQ));
@@ -1554,25 +1085,6 @@ void attn_dq_kernel(BwdParams p) {
             const int Lq = LrQ;
 #pragma unroll
             for (int kb = 0; kb < NKB; ++kb) sa[kb] = f32x16{};
-            if constexpr (DTA_DQ_AHEAD && NSQ * (NKB + 1) <= 12) {
-              // every operand read of this branch's S^T ahead of its MFMA chain (as in attn_fwd_kernel)
-              frag kfr[NKB][NSQ], qfr[NSQ];
-#pragma unroll
-              for (int s = 0; s < NSQ; ++s) {
-                if (i < NQR) qfr[s] = qf[i < NQR ? i : 0][s];
-                else qfr[s] = *reinterpret_cast<const frag*>(qbase + (Lq ^ (32 * s)));
-#pragma unroll
-                for (int kb = 0; kb < NKB; ++kb)
-                  kfr[kb][s] = *reinterpret_cast<const frag*>(kbase + kb * 32 * KI::ROWB + (Lr ^ (32 * s)));
-              }
-#pragma unroll
-              for (int s = 0; s < NSQ; ++s)
-#pragma unroll
-                for (int kb = 0; kb < NKB; ++kb) sa[kb] = O::mma(kfr[kb][s], qfr[s], sa[kb]);
-              if (i < NQR) __builtin_amdgcn_sched_group_barrier(0x100, NSQ * NKB, 0);
-              else __builtin_amdgcn_sched_group_barrier(0x100, NSQ * (NKB + 1), 0);
-              __builtin_amdgcn_sched_group_barrier(0x008, NSQ * NKB, 0);
-            } else {
 #pragma unroll
             for (int s = 0; s < NSQ; ++s) {
               frag qb;
@@ -1586,7 +1098,6 @@ void attn_dq_kernel(BwdParams p) {
                 else
                   sa[kb] = O::mma(*reinterpret_cast<const frag*>(kbase + kb * 32 * KI::ROWB + (Lr ^ (32 * s))), qb, sa[kb]);
               }
-            }
             }
           } else {
 #pragma unroll
@@ -1712,33 +1223,8 @@ struct TileRing {
     const int i = min(e / BQ, N - 1), r = e % BQ;
     return (uint32_t)((i * (uint32_t)bstride + r) * 4);
   }
-  // gq / gdo: (b, h) bases; lse / delta: (b, h) row-vector bases of branch 0.
-  // Wave w issues pieces j = u * NW + w; a slot u whose NW pieces are all of one
-  // kind is resolved at compile time (no per-piece scalar branching).
-  // slots [UA, UB) of this wave's pieces (the whole tile by default)
-  template <int UA = 0, int UB = MYP>
-  __device__ static void issue(const BwdParams& p, const E* gq, const E* gdo, const float* lse, const float* delta,
-                               int64_t bstride, int q0, int T, char* st0, int wave, int lane) {
-    const int rows = T - q0;                       // > 0 for every issued tile
-    const E* bq = gq + (int64_t)q0 * p.q.st;
-    const E* bd = gdo + (int64_t)q0 * p.dout.st;
-    const uint32_t nq = (uint32_t)rows * (uint32_t)(p.q.st * ES), nd = (uint32_t)rows * (uint32_t)(p.dout.st * ES);
-    const uint32_t nl = (uint32_t)(((N - 1) * bstride + rows) * 4);
-    sfor<(UB > UA ? UB - UA : 0)>([&](auto U) {
-      constexpr int u = UA + decltype(U)::value;
-      const int j = u * NW + wave;
-      if constexpr ((u + 1) * NW <= PQ) {
-        buf_lds16(bq, nq, st0 + j * 1024, offq(p, j, lane));
-      } else if constexpr (u * NW >= PQ && (u + 1) * NW <= PQ + PD) {
-        buf_lds16(bd, nd, st0 + OFF_D + (j - PQ) * 1024, offd(p, j, lane));
-      } else {
-        if (j < PQ) buf_lds16(bq, nq, st0 + j * 1024, offq(p, j, lane));
-        else if (j < PQ + PD) buf_lds16(bd, nd, st0 + OFF_D + (j - PQ) * 1024, offd(p, j, lane));
-        else if (j < PQ + PD + PL) buf_lds4(lse + q0, nl, st0 + OFF_L + (j - PQ - PD) * 256, offr(j, lane, bstride));
-        else if (j < NPC) buf_lds4(delta + q0, nl, st0 + OFF_G + (j - PQ - PD - PL) * 256, offr(j, lane, bstride));
-      }
-    });
-  }
+  // Wave w issues pieces j = u * NW + w; a slot u whose NW pieces are all of one kind
+  // is resolved at compile time (no per-piece scalar branching).
   // per-lane source offsets of this wave's pieces: the same for every tile (VGPRs, once)
   __device__ static void offsets(const BwdParams& p, int64_t bstride, int wave, int lane, uint32_t (&off)[MYP]) {
     sfor<MYP>([&](auto U) {
@@ -1749,6 +1235,7 @@ struct TileRing {
       else off[u] = j < PQ ? offq(p, j, lane) : (j < PQ + PD ? offd(p, j, lane) : (j < NPC ? offr(j, lane, bstride) : 0u));
     });
   }
+  // gq / gdo: (b, h) bases; lse / delta: (b, h) row-vector bases of branch 0
   __device__ static void issue_pre(const BwdParams& p, const E* gq, const E* gdo, const float* lse, const float* delta,
                                    int64_t bstride, int q0, int T, char* st0, int wave, const uint32_t (&off)[MYP]) {
     const int rows = T - q0;
@@ -1792,20 +1279,12 @@ struct DkdvCfg {
   static constexpr int LIMB = PR ? 80 * 1024 : 160 * 1024;     // PR: paired 4-wave plan, two per CU
   static constexpr int BK = NW * 32;
   static constexpr int HSP = HS < 32 ? 32 : HS;
-  // 64-row query stages (two 32-row sub-tiles per DMA round and barrier; 16-bit,
-  // DTA_DKDV_BQ = 64, the default) when K rows plus a 2-stage ring of them fit LDS;
-  // otherwise 32 (keeps the key block as wide as with 32-row stages)
-  static constexpr int BQ = (DTA_DKDV_BQ == 64 && sizeof(E) == 2 && HS >= 32 &&
-                             (N * BK * HS + 2 * (N * 64 * HSP + 64 * DV)) * (int)sizeof(E) +
-                                     2 * 2 * ((N * 64 + 63) / 64 * 64) * 4 <= LIMB) ? 64 : 32;
+  static constexpr int BQ = 32;                            // query rows per ring stage
   static constexpr int NP = (N * BQ + 63) / 64 * 64;      // fp32 row vectors, padded to DMA pieces
   static constexpr int nQ = N * BQ * HSP;
   static constexpr int nD = BQ * DV;
   static constexpr int nK = N * BK * HS;                   // the workgroup's K_i rows (B of S_i)
-  // the stagger (DTA_DKDV_STAGGER) holds one stage longer: take a fifth when it fits
-  static constexpr int NS0 = ring_stages_lim(nK * (int)sizeof(E), (nQ + nD) * (int)sizeof(E) + 2 * NP * 4, LIMB);
-  static constexpr int NS = (DTA_DKDV_STAGGER && NS0 == 4 &&
-                             nK * (int)sizeof(E) + 5 * ((nQ + nD) * (int)sizeof(E) + 2 * NP * 4) <= 160 * 1024) ? 5 : NS0;
+  static constexpr int NS = ring_stages_lim(nK * (int)sizeof(E), (nQ + nD) * (int)sizeof(E) + 2 * NP * 4, LIMB);
   static constexpr int bytes = (nK + NS * nQ + NS * nD) * (int)sizeof(E) + NS * 2 * NP * 4;
 };
 
@@ -1828,9 +1307,9 @@ struct DkdvWaves {
                              : (N * HSP / 2 + DV / 4 > DV / 2 ? N * HSP / 2 + DV / 4 : DV / 2) + 88;
   static constexpr int v8 = (sizeof(E) == 2 && DkdvCfg<E, HS, N, DV, 8>::bytes <= LIM && regs8 <= 256) ? 8
                           : DkdvCfg<E, HS, N, DV, 4>::bytes <= LIM ? 4 : 2;
-  // DTA_DKDV_PAIR (default): where the 8-wave plan applies, two 4-wave workgroups per CU instead
+  // paired plan: where the 8-wave plan applies, two 4-wave workgroups per CU instead
   // (bf16 only: the fp16 paired instantiation spills 16 VGPRs)
-  static constexpr bool pair = !NP && DTA_DKDV_PAIR && std::is_same<E, __bf16>::value && v8 == 8 &&
+  static constexpr bool pair = !NP && std::is_same<E, __bf16>::value && v8 == 8 &&
                                DkdvCfg<E, HS, N, DV, 4, true>::bytes <= 80 * 1024;
   static constexpr int v = pair ? 4 : v8;
 };
@@ -1858,7 +1337,6 @@ void attn_dkdv_kernel(BwdParams p) {
   float* Gb = Lb + NS * NP;                                 // [NS][NP] delta
   // SRD: the ring is instead NS stages of TileRing's layout, filled by buffer_load ... lds
   using RG = TileRing<E, HS, N, DV, NW, DK, BQ>;
-  constexpr int SUB = BQ / 32;            // 32-row sub-tiles per stage
   char* ringb = reinterpret_cast<char*>(Qb);
   static_assert(!SRD || (RG::ok && RG::SB * NS <= CF::bytes - CF::nK * (int)sizeof(E)), "ring layout");
 
@@ -1899,13 +1377,12 @@ void attn_dkdv_kernel(BwdParams p) {
       vf[s] = krow < T ? O::load_global(gv + (int64_t)krow * p.v.st + s * KS + hf * O::KH) : O::zero();
   }
 
-  uint32_t roff[SRD && DTA_DKDV_PREOFF ? RG::MYP : 1];
-  if constexpr (SRD && DTA_DKDV_PREOFF) RG::offsets(p, bstride, wave, lane, roff);
+  // per-lane DMA source offsets of this wave's pieces, computed once (VGPRs)
+  uint32_t roff[SRD ? RG::MYP : 1];
+  if constexpr (SRD) RG::offsets(p, bstride, wave, lane, roff);
   auto stage_q = [&](int q0, int buf) {
-    if constexpr (SRD && DTA_DKDV_PREOFF) {
+    if constexpr (SRD) {
       RG::issue_pre(p, gq, gdo, p.lse + rowvec, p.delta + rowvec, bstride, q0, T, ringb + buf * RG::SB, wave, roff);
-    } else if constexpr (SRD) {
-      RG::issue(p, gq, gdo, p.lse + rowvec, p.delta + rowvec, bstride, q0, T, ringb + buf * RG::SB, wave, lane);
     } else {
 #pragma unroll
       for (int i = 0; i < N; ++i)
@@ -1931,62 +1408,22 @@ void attn_dkdv_kernel(BwdParams p) {
   const int tile_pieces = SRD ? RG::pieces(wave)
                               : N * stage_pieces<E, HSP, BQ, HS, NW>(wave) + stage_pieces<E, DV, BQ, DV, NW>(wave) +
                                     rows_pieces<N, BQ, NW>(wave) * (DK ? 2 : 1);
-  // DTA_DKDV_STAGGER: waves 4-7 (the second wave on each SIMD) run their dV product
-  // of tile t at the start of step t+1, so the two waves sharing a SIMD are shifted
-  // by one MFMA block and one's softmax VALU meets the other's MFMAs instead of the
-  // pair running in lockstep (MI355X_MICROARCH.md, two waves per SIMD, item 9).
-  // Their dO tile t is still read in step t+1, so the ring prefetches one tile less
-  // far ahead (LA = NS - 2): the slot refilled in step t held tile t-2, released by
-  // every wave at the barrier closing step t-1.
-  constexpr bool STG = DTA_DKDV_STAGGER && NW == 8 && DVV && sizeof(E) == 2 && NS >= 3 && SUB == 1;
-  constexpr int LA = STG ? NS - 2 : NS - 1;
-  const bool g1 = STG && wave >= NW / 2;
-  for (int j = 0; j < LA; ++j)
+  for (int j = 0; j < NS - 1; ++j)
     if (j < ntiles) stage_q(kb0 + j * BQ, j);
-  wait_vm(tile_pieces * max(0, min(LA, ntiles) - 1));
+  wait_vm(tile_pieces * max(0, min(NS - 1, ntiles) - 1));
   lds_barrier();
   // K_i rows scaled once by scale*log2e in place, so S'_i = Q_i (sl2 K_i)^T; the S
   // accumulators start at the tile's -LSE rows and P = exp2(S'_i) needs no fma
   scale_lds<E, NTHR>(Ks, CF::nK, p.sl2, tid);
   lds_barrier();
   const bool wave_keys = kw0 < T;
-  // dV += (sum_i c_i P_i)^T dO of one tile from its packed P sums
-  auto dv_update = [&](const frag& p0, const frag& p1, const E* Dc) {
-    if constexpr (DVV && sizeof(E) == 2) {
-      const unsigned db = lds_addr(Dc);
-      const int Ld = tr_lane<DI::ROWB>(lane);
-      constexpr int NP2 = NVB >= 2 ? 2 : 1;       // d-blocks per LDS read batch
-      sfor<NVB / NP2>([&](auto D2) {
-        constexpr int d0 = NP2 * decltype(D2)::value;
-        lds64 r[NP2][4];
-        sfor<NP2>([&](auto E2) {
-          constexpr int d = d0 + decltype(E2)::value;
-          tr_issue<DI::ROWB, 0>(r[decltype(E2)::value], db + (Ld ^ (64 * d)), db + (Ld ^ (64 * d + 32)));
-        });
-        lgkm_pin<NP2>(r);
-#pragma unroll
-        for (int e = 0; e < NP2; ++e) {
-          dv[d0 + e] = O::mma(tr_frag<E>(r[e], 0), p0, dv[d0 + e]);
-          dv[d0 + e] = O::mma(tr_frag<E>(r[e], 1), p1, dv[d0 + e]);
-        }
-      });
-    }
-  };
-  auto slot_d = [&](int t) {
-    return SRD ? reinterpret_cast<const E*>(ringb + (t % NS) * RG::SB + RG::OFF_D) : Db + (t % NS) * BQ * DV;
-  };
-  frag pv0 = O::zero(), pv1 = O::zero();         // STG: waves 4-7's deferred P sums
-  bool pv_has = false;
-  // static priority for the second-dispatched half (MI355X_MICROARCH.md, two waves per SIMD, item 4)
-  if (NW == 8 && p.prio && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
 
   // masked diagonal tiles, unmasked interior, masked ragged tail tile; each loop
   // is one straight-line body (both variants behind a branch spill).  Lanes with
   // key >= T only pollute their own (never stored) dK/dV columns.
   Stamps st;
-  // per-lane LDS read bases, one register each across the loop (DTA_DKDV_LBASE): every
-  // read of a step is then one v_xad (base ^ k-step) + stage; without the switch they
-  // are re-derived from the lane id each step
+  // per-lane LDS read bases, one register each across the loop: every read of a step
+  // is then one v_xad (base ^ k-step) + stage
   int LrD = 0, LrQ = 0, LrK = 0, LtQ = 0, LtD = 0;
   // XA: the stage base is added to each family's lane base once per step and the
   // k-step / d-block XOR applied after it (valid: stage bases are multiples of XM, a
@@ -1994,8 +1431,8 @@ void attn_dkdv_kernel(BwdParams p) {
   // (The dynamic LDS array starts at address 0: the kernel has no static LDS.)
   constexpr int XMAX = 64 * ((NVB > NHB ? NVB : NHB) - 1) + 32 + 32 * ((NSV > NSQ ? NSV : NSQ) - 1);
   constexpr int XM = XMAX < 256 ? 256 : (XMAX < 512 ? 512 : 1024);
-  constexpr bool XA = DTA_DKDV_LBASE && SRD && sizeof(E) == 2 && SUB == 1 && !STG &&
-                      (CF::nK * (int)sizeof(E)) % XM == 0 && RG::SB % XM == 0 && QI::ROWB == KI::ROWB;
+  constexpr bool XA = SRD && sizeof(E) == 2 && (CF::nK * (int)sizeof(E)) % XM == 0 && RG::SB % XM == 0 &&
+                      QI::ROWB == KI::ROWB;
   if constexpr (sizeof(E) == 2) {
     LrD = row_lane<DI::ROWB>(lane); LrQ = row_lane<QI::ROWB>(lane); LrK = row_lane<KI::ROWB>(lane);
     LtQ = tr_lane<QI::ROWB>(lane); LtD = tr_lane<DI::ROWB>(lane);
@@ -2005,61 +1442,23 @@ void attn_dkdv_kernel(BwdParams p) {
     // keep lane-derived addresses loop-variant: recomputed per tile instead of
     // hoisted into (spilled) registers across the whole loop
     asm volatile("" : "+v"(lane));
-    if constexpr (DTA_DKDV_LBASE && sizeof(E) == 2) {
+    if constexpr (sizeof(E) == 2) {
       asm volatile("" : "+v"(LrD), "+v"(LrQ), "+v"(LtQ), "+v"(LtD));
       if constexpr (QI::ROWB == KI::ROWB) LrK = LrQ;     // same row pitch (HS >= 32)
       else asm volatile("" : "+v"(LrK));
-    } else if constexpr (sizeof(E) == 2) {
-      LrD = row_lane<DI::ROWB>(lane); LrQ = row_lane<QI::ROWB>(lane); LrK = row_lane<KI::ROWB>(lane);
-      LtQ = tr_lane<QI::ROWB>(lane); LtD = tr_lane<DI::ROWB>(lane);
     }
     tid = (wave << 6) + lane; hf = lane >> 5; c32 = lane & 31;
     krow = kw0 + c32;
     const int buf = t % NS;
     const int q0 = kb0 + t * BQ;
-    if constexpr (STG) {
-      if (pv_has) {                               // (g1 only) last step's deferred dV
-        dv_update(pv0, pv1, slot_d(t - 1));
-        pv_has = false;
-      }
-    }
-    // DTA_DKDV_SPLIT: this wave's DMA pieces for tile t+NS-1 go out in three parts
-    // spread over the step (after the barrier, after branch 0's S chain, before dV)
-    // instead of all at once, so 8 waves do not queue their pieces together
-    constexpr bool SPLIT = DTA_DKDV_SPLIT && SRD && !DTA_DKDV_PREOFF && RG::MYP >= 2 && !STG && SUB == 1;
-    const bool iss = t + LA < ntiles;
-    auto issue_part = [&](auto UA, auto UB) {
-      if (iss)
-        RG::template issue<decltype(UA)::value, decltype(UB)::value>(
-            p, gq, gdo, p.lse + rowvec, p.delta + rowvec, bstride, q0 + (NS - 1) * BQ, T,
-            ringb + ((t + NS - 1) % NS) * RG::SB, wave, lane);
-    };
-    using U0 = std::integral_constant<int, 0>;
-    using U1 = std::integral_constant<int, 1>;
-    using U2 = std::integral_constant<int, (SPLIT && RG::MYP >= 3) ? 2 : 1>;
-    using UM = std::integral_constant<int, RG::MYP>;
-    if constexpr (SPLIT) issue_part(U0{}, U1{});
-    else if (!DTA_DKDV_LATE && iss) stage_q(q0 + LA * BQ, (t + LA) % NS);
+    if (t + NS - 1 < ntiles) stage_q(q0 + (NS - 1) * BQ, (t + NS - 1) % NS);
     st.lap<0>();
-    const bool busy = wave_keys && q0 + BQ - 1 >= kw0;
-    if constexpr (SPLIT) if (!busy) issue_part(U1{}, UM{});
-    // BQ = 64: a stage holds two 32-row sub-tiles, computed one after the other with
-    // the same registers, so one DMA round, one wait and one barrier serve 64 rows
-    sfor<SUB>([&](auto USUB) {
-    constexpr int so = 32 * decltype(USUB)::value;
-    const int qs = q0 + so;                 // this sub-tile's first query row
-    if constexpr (SUB > 1) {
-      __builtin_amdgcn_sched_barrier(0);    // sub-tiles never interleave (registers)
-      asm volatile("" : "+v"(lane));        // and re-derive the lane addresses per sub-tile
-      hf = lane >> 5; c32 = lane & 31;
-      krow = kw0 + c32;
-    }
-    if (wave_keys && qs + 31 >= kw0) {
+    if (wave_keys && q0 + 31 >= kw0) {
       const char* sg = ringb + buf * RG::SB;
-      const E* Qc = (SRD ? reinterpret_cast<const E*>(sg) : Qb + buf * N * BQ * HSP) + so * HSP;
-      const E* Dc = (SRD ? reinterpret_cast<const E*>(sg + RG::OFF_D) : Db + buf * BQ * DV) + so * DV;
-      const float* Lc = (SRD ? reinterpret_cast<const float*>(sg + RG::OFF_L) : Lb + buf * NP) + so;
-      const float* Gc = (SRD ? reinterpret_cast<const float*>(sg + RG::OFF_G) : Gb + buf * NP) + so;
+      const E* Qc = SRD ? reinterpret_cast<const E*>(sg) : Qb + buf * N * BQ * HSP;
+      const E* Dc = SRD ? reinterpret_cast<const E*>(sg + RG::OFF_D) : Db + buf * BQ * DV;
+      const float* Lc = SRD ? reinterpret_cast<const float*>(sg + RG::OFF_L) : Lb + buf * NP;
+      const float* Gc = SRD ? reinterpret_cast<const float*>(sg + RG::OFF_G) : Gb + buf * NP;
       unsigned bQ = 0, bD = 0, tQ = 0, tD = 0;
       if constexpr (XA) {
         const unsigned sb = lds_addr(sg);
@@ -2095,8 +1494,8 @@ void attn_dkdv_kernel(BwdParams p) {
       st.lap<1>();
       f32x16 pc = f32x16{};
       // rows q0 + rowof(r) > lim are masked: query < key, or past the end
-      const int lim_lo = krow - qs - 4 * hf;          // masked if rowof_c < lim_lo (query < key)
-      const int lim_hi = T - 1 - qs - 4 * hf;         // masked if rowof_c > lim_hi (query >= T)
+      const int lim_lo = krow - q0 - 4 * hf;          // masked if rowof_c < lim_lo (query < key)
+      const int lim_hi = T - 1 - q0 - 4 * hf;         // masked if rowof_c > lim_hi (query >= T)
 #pragma unroll
       for (int i = 0; i < N; ++i) {
         // S'_i accumulator seeded with the -LSE rows (K_i is pre-scaled by sl2)
@@ -2129,7 +1528,6 @@ void attn_dkdv_kernel(BwdParams p) {
           for (int s = 0; s < NSQ; ++s)
             sa = O::mma(QI::row(Qi, c32, s, hf), KI::row(Ks + i * BK * HS, wave * 32 + c32, s, hf), sa);
         }
-        if constexpr (SPLIT) if (i == 0) issue_part(U1{}, U2{});
         // sa[r] = S'_i[q0 + rowof(r)][krow] - LSE; rows 4g..4g+3 of a lane are consecutive
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
@@ -2146,7 +1544,7 @@ void attn_dkdv_kernel(BwdParams p) {
             const float pr = exp2_fast(arg);
             if constexpr (DROP) {
               // this map element's kept weight mask/(1-p)
-              const float mk = drop_mul(dkey[i], qs + (r & 3) + 8 * (r >> 2) + 4 * hf, krow, p.drop_thr, p.drop_scale);
+              const float mk = drop_mul(dkey[i], q0 + (r & 3) + 8 * (r >> 2) + 4 * hf, krow, p.drop_thr, p.drop_scale);
               if constexpr (DVV) pc[r] = fmaf(coef[i] * mk, pr, pc[r]);
               if constexpr (DK) sa[r] = pr * fmaf(mk, dpa[r], -d4[j]);
             } else {
@@ -2181,16 +1579,7 @@ void attn_dkdv_kernel(BwdParams p) {
         }
       }
       st.lap<2>();
-      if constexpr (SPLIT) issue_part(U2{}, UM{});
-      if constexpr (STG) {
-        if (g1) {
-          pv0 = O::template pack<0>(pc);
-          pv1 = O::template pack<1>(pc);
-          pv_has = true;
-        } else {
-          dv_update(O::template pack<0>(pc), O::template pack<1>(pc), Dc);
-        }
-      } else if constexpr (DVV) {
+      if constexpr (DVV) {
         if constexpr (sizeof(E) == 2) {
           const unsigned db = lds_addr(Dc);
           const int Ld = LtD;
@@ -2220,11 +1609,8 @@ void attn_dkdv_kernel(BwdParams p) {
       }
       }
     }
-    });
-    // DTA_DKDV_LATE: the next tile's DMA goes out after the compute, beside the barrier wait
-    if constexpr (DTA_DKDV_LATE && !SPLIT) if (iss) stage_q(q0 + LA * BQ, (t + LA) % NS);
     st.lap<3>();
-    wait_vm(tile_pieces * max(0, min(LA - 1, ntiles - 2 - t)));
+    wait_vm(tile_pieces * max(0, min(NS - 2, ntiles - 2 - t)));
     st.lap<4>();
     lds_barrier();
     st.lap<5>();
@@ -2235,8 +1621,6 @@ void attn_dkdv_kernel(BwdParams p) {
   for (int t = 0; t < thead; ++t) step(t, std::true_type{});
   for (int t = thead; t < ttail; ++t) step(t, std::false_type{});
   for (int t = ttail; t < ntiles; ++t) step(t, std::true_type{});
-  if constexpr (STG)
-    if (pv_has) dv_update(pv0, pv1, slot_d(ntiles - 1));   // no DMA refills this slot any more
   st.flush(p.stamps, lin * NW + wave, lane);
 
   if (!wave_keys || krow >= T) return;
@@ -2271,298 +1655,6 @@ void attn_dkdv_kernel(BwdParams p) {
   }
 }
 
-// ------------------------------------ backward: dK, dV, one wave per SIMD ---
-//
-// Same math and operand maps as attn_dkdv_kernel, re-planned for the 512-entry
-// register file of a single wave per SIMD (4-wave workgroup, 128 keys):
-//  * K_i and V key rows live in registers for the whole loop (B operands of S_i
-//    and dP), so the only LDS reads per query tile are the streamed Q_i / dO /
-//    LSE / c*delta and their transposed reads;
-//  * every per-lane LDS and global offset is computed once, before the loop;
-//  * tiles arrive by buffer_load ... lds through per-tile buffer descriptors built
-//    in SGPRs (row base and byte extent), so a tile costs no vector address math
-//    and rows past T read as zeros (then masked) instead of being clamped.
-template <class E, int HS, int N, int DV>
-struct Dkdv4Cfg {
-  static constexpr int NW = 4, BQ = 64, BK = NW * 32, NS = 3;
-  using R = TileRing<E, HS, N, DV, NW, true, BQ>;
-  static constexpr int bytes = NS * R::SB;
-  // rough register count: dK/dV accumulators, K/V fragments, two 32-row sub-tiles of scores / operands
-  static constexpr int regs = N * HS / 2 + DV / 2 + DV / 4 + N * HS / 4 +      // dk, dv, vf, kf
-                              2 * (N * 16 + 16 + N * 16) +                       // sa, dpa, delta rows
-                              N * HS / 4 + DV / 4 + 2 * (N + 1) * 8 + 48;        // operand rows, packs, misc
-  static constexpr bool ok = R::ok && HS <= 64 && bytes <= 160 * 1024 && regs <= 520;
-};
-
-// One wave per SIMD: 4 waves x 32 keys; each step consumes a 64-row query tile as
-// two 32-row sub-tiles whose MFMA chains and softmax VALU are independent, so the
-// scheduler can run one sub-tile's VALU beside the other's MFMAs.
-//  * K_i (pre-multiplied by scale*log2e, once) and V rows stay in registers;
-//  * the S accumulators start at the stored -LSE rows, so P = exp2(S') directly;
-//  * tiles arrive through TileRing (descriptor-based LDS-DMA, no per-tile vector math).
-template <class E, int HS, int N, int DV>
-__global__ __launch_bounds__(256, 1) void attn_dkdv4_kernel(BwdParams p) {
-  using O = Ops<E>;
-  using frag = typename O::frag;
-  using CF = Dkdv4Cfg<E, HS, N, DV>;
-  using R = typename CF::R;
-  constexpr int BQ = CF::BQ, BK = CF::BK, NS = CF::NS, SB = R::SB;
-  constexpr int QB = R::QB, OFF_D = R::OFF_D, OFF_L = R::OFF_L, OFF_G = R::OFF_G;
-  using QI = Img<E, HS>;
-  using DI = Img<E, DV>;
-  constexpr int KS = O::KSTEP;
-  constexpr int NSQ = HS / KS, NSV = DV / KS, NHB = HS / 32, NVB = DV / 32;
-
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63, hf = lane >> 5, c32 = lane & 31;
-  const int nblk = gridDim.x * gridDim.y * gridDim.z;
-  const int lin = xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z), nblk);
-  const int kblk = lin % gridDim.x, hh = (lin / gridDim.x) % gridDim.y, b = lin / (gridDim.x * gridDim.y);
-  const int T = p.T;
-  const int kb0 = kblk * BK, kw0 = kb0 + wave * 32;
-  const int krow = kw0 + c32;
-
-  const E* gq = reinterpret_cast<const E*>(p.q.p) + b * p.q.sb + hh * p.q.sh;
-  const E* gk = reinterpret_cast<const E*>(p.k.p) + b * p.k.sb + hh * p.k.sh;
-  const E* gv = reinterpret_cast<const E*>(p.v.p) + b * p.v.sb + hh * p.v.sh;
-  const E* gdo = reinterpret_cast<const E*>(p.dout.p) + b * p.dout.sb + hh * p.dout.sh;
-  const int64_t rowvec = ((int64_t)b * p.H + hh) * T;
-  const int64_t bstride = (int64_t)p.B * p.H * T;
-
-  float coef[N];
-#pragma unroll
-  for (int i = 0; i < N; ++i) coef[i] = p.coef[hh * N + i];
-
-  // this wave's key rows: sl2 * K_i (B of S'_i = Q_i (sl2 K_i)^T) and V (B of dP = dO V^T)
-  frag kf[N][NSQ], vf[NSV];
-#pragma unroll
-  for (int i = 0; i < N; ++i)
-#pragma unroll
-    for (int s = 0; s < NSQ; ++s) {
-      frag k = krow < T ? O::load_global(gk + (int64_t)krow * p.k.st + i * p.k.si + s * KS + hf * O::KH) : O::zero();
-#pragma unroll
-      for (int j = 0; j < 8; ++j) k[j] = (E)((float)k[j] * p.sl2);
-      kf[i][s] = k;
-    }
-#pragma unroll
-  for (int s = 0; s < NSV; ++s)
-    vf[s] = krow < T ? O::load_global(gv + (int64_t)krow * p.v.st + s * KS + hf * O::KH) : O::zero();
-
-  const int mypieces = R::pieces(wave);
-  const int ntiles = kb0 < T ? (T - kb0 + BQ - 1) / BQ : 0;
-  auto stage = [&](int t, int buf) {
-    R::issue(p, gq, gdo, p.lse + rowvec, p.delta + rowvec, bstride, kb0 + t * BQ, T, smem + buf * SB, wave, lane);
-  };
-
-  // loop-invariant LDS read offsets (bytes within a stage, sub-tile 0)
-  uint32_t lq[NSQ], ld[NSV], tq[NHB][2], td[NVB][2];
-  {
-    const int Lq = row_lane<QI::ROWB>(lane), Ld = row_lane<DI::ROWB>(lane);
-    const int Tq = tr_lane<QI::ROWB>(lane), Td = tr_lane<DI::ROWB>(lane);
-#pragma unroll
-    for (int s = 0; s < NSQ; ++s) lq[s] = Lq ^ (32 * s);
-#pragma unroll
-    for (int s = 0; s < NSV; ++s) ld[s] = OFF_D + (Ld ^ (32 * s));
-#pragma unroll
-    for (int d = 0; d < NHB; ++d) { tq[d][0] = Tq ^ (64 * d); tq[d][1] = Tq ^ (64 * d + 32); }
-#pragma unroll
-    for (int d = 0; d < NVB; ++d) { td[d][0] = OFF_D + (Td ^ (64 * d)); td[d][1] = OFF_D + (Td ^ (64 * d + 32)); }
-  }
-  const int lrow = 16 * hf;          // + 32 g bytes: rows 8g + 4hf of a 32-row vector
-
-  f32x16 dk[N][NHB], dv[NVB];
-#pragma unroll
-  for (int i = 0; i < N; ++i)
-#pragma unroll
-    for (int d = 0; d < NHB; ++d) dk[i][d] = f32x16{};
-#pragma unroll
-  for (int d = 0; d < NVB; ++d) dv[d] = f32x16{};
-  // dK / dV accumulators belong in AGPRs (only MFMAs touch them); the per-tile
-  // score accumulators in VGPRs, where the softmax VALU reads them
-  auto pin_acc = [&]() {
-#pragma unroll
-    for (int i = 0; i < N; ++i)
-#pragma unroll
-      for (int d = 0; d < NHB; ++d) asm volatile("" : "+a"(dk[i][d]));
-#pragma unroll
-    for (int d = 0; d < NVB; ++d) asm volatile("" : "+a"(dv[d]));
-    // K / V fragments are MFMA B operands only: AGPRs too
-#pragma unroll
-    for (int i = 0; i < N; ++i)
-#pragma unroll
-      for (int s = 0; s < NSQ; ++s) asm volatile("" : "+a"(kf[i][s]));
-#pragma unroll
-    for (int s = 0; s < NSV; ++s) asm volatile("" : "+a"(vf[s]));
-  };
-  pin_acc();
-
-  for (int j = 0; j < NS - 1; ++j)
-    if (j < ntiles) stage(j, j);
-  wait_vm(mypieces * max(0, min(NS - 1, ntiles) - 1));
-  lds_barrier();
-  const bool wave_keys = kw0 < T;
-  const unsigned sbase = lds_addr(smem);
-
-  auto step = [&](int t, auto MASKED) {
-    constexpr bool MASK = decltype(MASKED)::value;
-    const int buf = t % NS;
-    const int q0 = kb0 + t * BQ;
-    if (t + NS - 1 < ntiles) stage(t + NS - 1, (t + NS - 1) % NS);
-    if (wave_keys && q0 + BQ - 1 >= kw0) {
-      const char* st0 = smem + buf * SB;
-      const unsigned sa0 = sbase + buf * SB;
-      // ---- MFMA chains of both sub-tiles: S'_i = -LSE_i + Q_i (sl2 K_i)^T, dP = dO V^T
-      f32x16 sa[2][N], dpa[2];
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        frag qr[N][NSQ], dr[NSV];
-#pragma unroll
-        for (int i = 0; i < N; ++i) {
-#pragma unroll
-          for (int s = 0; s < NSQ; ++s) qr[i][s] = *reinterpret_cast<const frag*>(st0 + i * QB + u * 32 * QI::ROWB + lq[s]);
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const f32x4 l4 = *reinterpret_cast<const f32x4*>(st0 + OFF_L + (i * BQ + 32 * u) * 4 + 32 * g + lrow);
-#pragma unroll
-            for (int jj = 0; jj < 4; ++jj) sa[u][i][4 * g + jj] = l4[jj];
-          }
-        }
-#pragma unroll
-        for (int s = 0; s < NSV; ++s) dr[s] = *reinterpret_cast<const frag*>(st0 + u * 32 * DI::ROWB + ld[s]);
-#pragma unroll
-        for (int i = 0; i < N; ++i)
-#pragma unroll
-          for (int s = 0; s < NSQ; ++s) sa[u][i] = O::mma(qr[i][s], kf[i][s], sa[u][i]);
-        // dP accumulator seeded with -delta_0 (attn_dq's row constants, see attn_dkdv_kernel)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const f32x4 g4 = *reinterpret_cast<const f32x4*>(st0 + OFF_G + (32 * u) * 4 + 32 * g + lrow);
-#pragma unroll
-          for (int jj = 0; jj < 4; ++jj) dpa[u][4 * g + jj] = g4[jj];
-        }
-#pragma unroll
-        for (int s = 0; s < NSV; ++s) dpa[u] = O::mma(dr[s], vf[s], dpa[u]);
-#pragma unroll
-        for (int i = 0; i < N; ++i) asm volatile("" : "+v"(sa[u][i]));
-        asm volatile("" : "+v"(dpa[u]));
-      }
-      // ---- softmax side per sub-tile: P_i = exp2(S'_i); pc = sum_i c_i P_i; dS_i / c_i = P_i (dP - delta_i)
-      frag pk[2][2], ds[2][N][2];
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int lim_lo = krow - q0 - 32 * u - 4 * hf;     // masked if row < lim_lo (query < key)
-        const int lim_hi = T - 1 - q0 - 32 * u - 4 * hf;    // masked if row > lim_hi (query >= T)
-        f32x16 pc;
-#pragma unroll
-        for (int i = 0; i < N; ++i) {
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            f32x4 d4 = f32x4{};
-            if (i > 0) d4 = *reinterpret_cast<const f32x4*>(st0 + OFF_G + (i * BQ + 32 * u) * 4 + 32 * g + lrow);
-#pragma unroll
-            for (int jj = 0; jj < 4; ++jj) {
-              const int r = 4 * g + jj;
-              float pr = exp2_fast(sa[u][i][r]);
-              if constexpr (MASK) {
-                const int rc = (r & 3) + 8 * (r >> 2);
-                pr = (rc < lim_lo || rc > lim_hi) ? 0.f : pr;
-              }
-              pc[r] = i == 0 ? coef[0] * pr : fmaf(coef[i], pr, pc[r]);
-              sa[u][i][r] = i == 0 ? pr * dpa[u][r] : pr * (dpa[u][r] + d4[jj]);   // dS_i / c_i
-            }
-          }
-          ds[u][i][0] = O::template pack<0>(sa[u][i]);
-          ds[u][i][1] = O::template pack<1>(sa[u][i]);
-        }
-        pk[u][0] = O::template pack<0>(pc);
-        pk[u][1] = O::template pack<1>(pc);
-      }
-      // ---- dV^T += dO^T pc (transposed dO reads, k = the 64 query rows)
-#pragma unroll
-      for (int d = 0; d < NVB; ++d) {
-        lds64 r[2][4];
-        tr_issue<DI::ROWB, 0>(r[0], sa0 + td[d][0], sa0 + td[d][1]);
-        tr_issue<DI::ROWB, 32>(r[1], sa0 + td[d][0], sa0 + td[d][1]);
-        lgkm_pin<2>(r);
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          dv[d] = O::mma(tr_frag<E>(r[u], 0), pk[u][0], dv[d]);
-          dv[d] = O::mma(tr_frag<E>(r[u], 1), pk[u][1], dv[d]);
-        }
-      }
-      // ---- dK_i^T += Q_i^T dS_i (transposed Q_i reads)
-#pragma unroll
-      for (int i = 0; i < N; ++i)
-#pragma unroll
-        for (int d = 0; d < NHB; ++d) {
-          lds64 r[2][4];
-          tr_issue<QI::ROWB, 0>(r[0], sa0 + i * QB + tq[d][0], sa0 + i * QB + tq[d][1]);
-          tr_issue<QI::ROWB, 32>(r[1], sa0 + i * QB + tq[d][0], sa0 + i * QB + tq[d][1]);
-          lgkm_pin<2>(r);
-#pragma unroll
-          for (int u = 0; u < 2; ++u) {
-            dk[i][d] = O::mma(tr_frag<E>(r[u], 0), ds[u][i][0], dk[i][d]);
-            dk[i][d] = O::mma(tr_frag<E>(r[u], 1), ds[u][i][1], dk[i][d]);
-          }
-        }
-    }
-    pin_acc();
-    wait_vm(mypieces * max(0, min(NS - 2, ntiles - 2 - t)));
-    lds_barrier();
-  };
-  const int thead = min(ntiles, (BK - 2) / BQ + 1);                    // q0 < kb0 + BK - 1
-  const int ttail = max(thead, ntiles - ((T - kb0) % BQ != 0 ? 1 : 0));  // q0 + BQ > T
-  for (int t = 0; t < thead; ++t) step(t, std::true_type{});
-  for (int t = thead; t < ttail; ++t) step(t, std::false_type{});
-  for (int t = ttail; t < ntiles; ++t) step(t, std::true_type{});
-
-  if (!wave_keys || krow >= T) return;
-  E* gdk = reinterpret_cast<E*>(p.dk.p) + b * p.dk.sb + (int64_t)krow * p.dk.st + hh * p.dk.sh;
-#pragma unroll
-  for (int i = 0; i < N; ++i)
-#pragma unroll
-    for (int d = 0; d < NHB; ++d)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int e = d * 32 + 8 * g + 4 * hf;
-        const float sc = p.scale * coef[i];
-        float a0 = dk[i][d][4 * g] * sc, a1 = dk[i][d][4 * g + 1] * sc;
-        float a2 = dk[i][d][4 * g + 2] * sc, a3 = dk[i][d][4 * g + 3] * sc;
-        if (p.rope) rope_inv4(p.rope, krow, HS, e, a0, a1, a2, a3);
-        store4<E>(gdk + i * p.dk.si + e, a0, a1, a2, a3);
-      }
-  E* gdv = reinterpret_cast<E*>(p.dv.p) + b * p.dv.sb + (int64_t)krow * p.dv.st + hh * p.dv.sh;
-#pragma unroll
-  for (int d = 0; d < NVB; ++d)
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int e = d * 32 + 8 * g + 4 * hf;
-      store4<E>(gdv + e, dv[d][4 * g], dv[d][4 * g + 1], dv[d][4 * g + 2], dv[d][4 * g + 3]);
-    }
-}
-
-// dK/dV kernel choice for A/B measurements: unset / DTA_DKDV=8 the 8-wave kernel
-// with descriptor staging, DTA_DKDV=4 the one-wave-per-SIMD kernel where its plan
-// fits, DTA_DKDV=0 the 8-wave kernel with address-computed staging.
-// DTA_KV_STAGING=0: forward / dQ kernels stage K and V by per-lane addresses
-// instead of buffer descriptors (A/B measurements)
-inline bool kv_staging() {
-  static const bool on = [] {
-    const char* s = getenv("DTA_KV_STAGING");
-    return !(s && s[0] == '0');
-  }();
-  return on;
-}
-
-inline int dkdv_mode() {
-  static const int m = [] {
-    const char* s = getenv("DTA_DKDV");
-    return s && s[0] == '4' ? 4 : (s && s[0] == '0' ? 0 : 8);
-  }();
-  return m;
-}
-
 // ------------------------------------------------------------ launchers ---
 template <class K>
 static inline int set_smem(K kernel, int bytes) {
@@ -2581,33 +1673,11 @@ struct Plan {
   static constexpr bool ok = FP::ok && DP::ok && DkdvCfg<E, HS, N, DV, KVW, KPR>::bytes <= 160 * 1024;
 };
 
-// forward kernel choice: DTA_FWD_PIPE=1 (env) or -DDTA_FWD_PIPE_DEFAULT=1 selects the
-// software-pipelined one-wave-per-SIMD kernel where its plan fits
-#ifndef DTA_FWD_PIPE_DEFAULT
-#define DTA_FWD_PIPE_DEFAULT 0
-#endif
-inline bool fwd_pipe() {
-  static const bool on = [] {
-    const char* s = getenv("DTA_FWD_PIPE");
-    return s ? s[0] == '1' : DTA_FWD_PIPE_DEFAULT != 0;
-  }();
-  return on;
-}
-
 template <class E, int HS, int N, int DV_, bool DROP>
 int launch_fwd_t(const FwdParams& p, hipStream_t st) {
   using PL = Plan<E, HS, N, DV_>;
   using FP = FwdPick<E, HS, N, PL::DV, DROP>;
   constexpr int DVC = FP::DVC, NW = FP::NW;
-  if constexpr (!DROP && FwdPipeCfg<E, HS, N, DVC>::ok) {
-    if (fwd_pipe() && kv_layout_ok(p, (int)sizeof(E))) {
-      using PC = FwdPipeCfg<E, HS, N, DVC>;
-      auto kern = attn_fwd_pipe_kernel<E, HS, N, DVC>;
-      if (int e = set_smem(kern, PC::bytes)) return e;
-      hipLaunchKernelGGL(kern, dim3((p.T + PC::BM - 1) / PC::BM, p.H * (PL::DV / DVC), p.B), dim3(256), PC::bytes, st, p);
-      return (int)hipGetLastError();
-    }
-  }
   constexpr int QH = FP::QH;
   constexpr int bytes = FwdCfg<E, HS, N, DVC, NW, FP::QREG, QH>::bytes;
   dim3 grid((p.T + NW * 32 - 1) / (NW * 32), p.H * (PL::DV / DVC), p.B);
@@ -2619,7 +1689,7 @@ int launch_fwd_t(const FwdParams& p, hipStream_t st) {
   };
   int e = 0;
   if constexpr (KvRing<E, HS, N, DVC, FwdCfg<E, HS, N, DVC, NW, FP::QREG, QH>::BN, NW>::ok)
-    e = kv_staging() && kv_layout_ok(p, (int)sizeof(E)) ? run(std::true_type{}) : run(std::false_type{});
+    e = kv_layout_ok(p, (int)sizeof(E)) ? run(std::true_type{}) : run(std::false_type{});
   else
     e = run(std::false_type{});
   if (e) return e;
@@ -2644,7 +1714,7 @@ int launch_dq_t(const BwdParams& p, hipStream_t st) {
   auto go = [&](auto SRDV) -> int { return p.dq32 ? run(std::true_type{}, SRDV) : run(std::false_type{}, SRDV); };
   int e = 0;
   if constexpr (KvRing<E, HS, N, DV, DqCfg<E, HS, N, DV, NW, QR, QH>::BN, NW>::ok && DqCfg<E, HS, N, DV, NW, QR, QH>::HSP == HS)
-    e = kv_staging() && kv_layout_ok(p, (int)sizeof(E)) ? go(std::true_type{}) : go(std::false_type{});
+    e = kv_layout_ok(p, (int)sizeof(E)) ? go(std::true_type{}) : go(std::false_type{});
   else
     e = go(std::false_type{});
   if (e) return e;
@@ -2656,15 +1726,6 @@ int launch_dkdv_t(const BwdParams& p, hipStream_t st) {
   using PL = Plan<E, HS, N, DV_>;
   using KW = DkdvWaves<E, HS, N, PL::DV, DROP>;
   constexpr int NW = KW::v, DV = PL::DV;
-  if constexpr (!DROP && Dkdv4Cfg<E, HS, N, DV>::ok) {
-    if (dkdv_mode() == 4 && ring_layout_ok(p, (int)sizeof(E))) {
-      using C4 = Dkdv4Cfg<E, HS, N, DV>;
-      auto kern = attn_dkdv4_kernel<E, HS, N, DV>;
-      if (int e = set_smem(kern, C4::bytes)) return e;
-      hipLaunchKernelGGL(kern, dim3((p.T + C4::BK - 1) / C4::BK, p.H, p.B), dim3(C4::NW * 64), C4::bytes, st, p);
-      return (int)hipGetLastError();
-    }
-  }
   constexpr bool PR = KW::pair;
   constexpr int bytes = DkdvCfg<E, HS, N, DV, NW, PR>::bytes;
   dim3 grid((p.T + NW * 32 - 1) / (NW * 32), p.H, p.B);
@@ -2687,7 +1748,7 @@ int launch_dkdv_t(const BwdParams& p, hipStream_t st) {
   };
   int e = 0;
   if constexpr (TileRing<E, HS, N, DV, NW, true, DkdvCfg<E, HS, N, DV, NW, PR>::BQ>::ok) {
-    e = dkdv_mode() != 0 && ring_layout_ok(p, (int)sizeof(E)) ? go(std::true_type{}) : go(std::false_type{});
+    e = ring_layout_ok(p, (int)sizeof(E)) ? go(std::true_type{}) : go(std::false_type{});
   } else {
     e = go(std::false_type{});
   }

@@ -125,16 +125,6 @@ bool ok_dims(int dtype, int B, int T, int H, int N, int hs, int dv) {
 
 }  // namespace
 
-// DTA_PRIO=1 gives the second wave half of 8-wave workgroups a static s_setprio 1
-// (A/B measurements; default off)
-static int wave_prio() {
-  static const int v = [] {
-    const char* e = getenv("DTA_PRIO");
-    return e && e[0] == '1' ? 1 : 0;
-  }();
-  return v;
-}
-
 #ifndef DTA_STAMPS
 #define DTA_STAMPS 0
 #endif
@@ -194,7 +184,6 @@ int dta_attn_fwd(const dta_attn_fwd_args* a, void* stream) {
   p.lse = a->lse; p.coef = a->coef;
   p.B = a->B; p.T = a->T; p.H = a->H; p.N = a->n_terms; p.HS = a->head_size; p.DV = a->dv;
   p.sl2 = a->scale * kLog2e;
-  p.prio = wave_prio();
   p.stamps = stamp_buf();
   return status(launch_attn_fwd(a->dtype, p, (hipStream_t)stream));
 }
@@ -239,7 +228,6 @@ int dta_attn_bwd(const dta_attn_bwd_args* a, void* stream) {
   p.dcoef_part = a->dcoef_partial;
   p.B = a->B; p.T = a->T; p.H = a->H; p.N = a->n_terms; p.HS = a->head_size; p.DV = a->dv;
   p.scale = a->scale; p.sl2 = a->scale * kLog2e;
-  p.prio = wave_prio();
   p.stamps = stamp_buf();
   int e = 0;
   if ((stages & DTA_BWD_DQ) && (e = launch_attn_dq(a->dtype, p, st))) return status(e);

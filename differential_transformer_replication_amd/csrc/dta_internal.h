@@ -17,7 +17,6 @@ struct FwdParams {
   const float* coef;
   int B, T, H, N, HS, DV;
   float sl2;           // scale * log2(e)
-  int prio;            // 1: waves 4-7 of an 8-wave workgroup run at s_setprio 1
   unsigned long long* stamps;   // diagnostic builds (DTA_STAMPS) only: per-wave segment cycle sums
   uint32_t drop_thr;   // attention dropout: keep iff hash >= drop_thr (= p * 2^32); 0 = off
   float drop_scale;    // 1 / (1 - p)
@@ -35,7 +34,6 @@ struct BwdParams {
   float* dcoef_part;   // if set: per-wave d(coef) partials [h][i][b][T/32] (no atomics), summed by dcoef_reduce
   int B, T, H, N, HS, DV;
   float sl2, scale;
-  int prio;            // as FwdParams::prio
   unsigned long long* stamps;   // as FwdParams::stamps
   uint32_t drop_thr;   // as FwdParams
   float drop_scale;

@@ -1,4 +1,4 @@
-# Build lib/libdiffattn_<name>.so: attn_bf16.hip compiled with extra flags (e.g. -DDTA_FWD_PINGPONG=1),
+# Build lib/libdiffattn_<name>.so: attn_bf16.hip compiled with extra flags (e.g. -DDTA_STAMPS=1),
 # everything else from the regular build.   bash tools/build_variant.sh <name> "<flags>"
 set -e
 NAME=$1; EXTRA=$2

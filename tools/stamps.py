@@ -20,7 +20,6 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 from differential_transformer_replication_amd import _lib  # noqa: E402
 
 FWD_SEGS = ["dma_issue", "qk_softmax", "pv", "wait_vm", "barrier", "tail", "-", "loop_top"]
-PIPE_SEGS = ["max_rescale", "dma_issue", "qk_next+exp+pv", "wait_vm", "barrier", "-", "-", "-"]
 DKDV_SEGS = ["dma_issue", "dP", "branches(S,dS,dK)", "dV", "wait_vm", "barrier", "-", "-"]
 
 
@@ -75,7 +74,7 @@ def main():
         assert lib.dta_debug_stamps(buf.ctypes.data, nbytes) == 0
         st = buf.reshape(-1, 8)
         st = st[st.sum(1) > 0].astype(np.float64)
-        names = (PIPE_SEGS if os.environ.get("DTA_FWD_PIPE") == "1" else FWD_SEGS) if which == "fwd" else DKDV_SEGS
+        names = FWD_SEGS if which == "fwd" else DKDV_SEGS
         tot = st.sum(0)
         out[which] = {"waves": int(st.shape[0]),
                       "share": {n: round(float(x / tot.sum()), 4) for n, x in zip(names, tot) if n != "-"},
