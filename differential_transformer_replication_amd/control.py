@@ -26,7 +26,7 @@ __all__ = ["precompute_freqs_cis", "apply_rotary_emb", "Head", "MultiHeadAttenti
 
 
 def _fused_ok(x: torch.Tensor, p: float, hs: int) -> bool:
-    # the fused kernels' standard-attention plans: head sizes 64 and 128 (dv = hs);
+    # the fused kernels' standard-attention plans (dv = hs: head sizes 64, 96, 128);
     # x.dtype is the projection's dtype under autocast too
     dt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else x.dtype
     return x.is_cuda and 0.0 <= p < 1.0 and ops.supported(dt, hs, 1, hs)

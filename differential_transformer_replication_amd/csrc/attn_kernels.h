@@ -73,6 +73,15 @@ struct Stamps {
 };
 
 // ------------------------------------------------------------ LDS images ---
+// Image width for a logical width: LDS rows keep a power-of-two pitch (the XOR
+// swizzle's domain), so head size 96 / value width 192 live in 128 / 256-column rows
+// whose pad columns are staged but never read.
+constexpr int img_cols(int c) {
+  int p = 1;
+  while (p < c) p <<= 1;
+  return p;
+}
+
 template <int ROWB>
 __device__ __forceinline__ int swz(int r) {
   if constexpr (ROWB >= 256) return ((r & 3) << 2) | ((r >> 2) & 3);
@@ -362,22 +371,28 @@ __device__ __forceinline__ void buf_lds4(const void* base, uint32_t bytes, char*
 template <class E, int HS, int N, int DVC, int BN, int NW>
 struct KvRing {
   static constexpr int ES = (int)sizeof(E);
-  static constexpr int KB = BN * HS * ES, VB = BN * DVC * ES;
+  static constexpr int HSP = img_cols(HS), DVP = img_cols(DVC);   // image widths
+  static constexpr int KB = BN * HSP * ES, VB = BN * DVP * ES;
   static constexpr int PK = N * KB / 1024, PV = VB / 1024, NPC = PK + PV;
   static constexpr int MYP = (NPC + NW - 1) / NW;
   static constexpr bool ok = ES == 2 && HS >= 32 && KB % 1024 == 0 && VB % 1024 == 0;
 
   __device__ static int pieces(int wave) { return NPC / NW + (wave < NPC % NW ? 1 : 0); }
+  // (pad chunks of a padded image read the row's first chunk: in bounds, never used)
   __device__ static uint32_t offk(int64_t st, int64_t si, int j, int lane) {
-    using KI = Img<E, HS>;
+    using KI = Img<E, HSP>;
     const int i = j / (KB / 1024), pb = (j % (KB / 1024)) * 1024 + lane * 16;
-    const int r = pb / KI::ROWB, c = ((pb % KI::ROWB) >> 4) ^ swz<KI::ROWB>(r);
+    const int r = pb / KI::ROWB;
+    int c = ((pb % KI::ROWB) >> 4) ^ swz<KI::ROWB>(r);
+    if constexpr (HSP != HS) c = c * 16 < HS * ES ? c : 0;
     return (uint32_t)(r * (uint32_t)(st * ES) + (uint32_t)(i * si * ES) + c * 16);
   }
   __device__ static uint32_t offv(int64_t st, int j, int lane) {
-    using VI = Img<E, DVC>;
+    using VI = Img<E, DVP>;
     const int pb = (j - PK) * 1024 + lane * 16;
-    const int r = pb / VI::ROWB, c = ((pb % VI::ROWB) >> 4) ^ swz<VI::ROWB>(r);
+    const int r = pb / VI::ROWB;
+    int c = ((pb % VI::ROWB) >> 4) ^ swz<VI::ROWB>(r);
+    if constexpr (DVP != DVC) c = c * 16 < DVC * ES ? c : 0;
     return (uint32_t)(r * (uint32_t)(st * ES) + c * 16);
   }
   // this wave's pieces of one tile, source offsets computed per tile
@@ -477,9 +492,10 @@ struct FwdCfg {
   static constexpr bool PAIR = NW == 4 && !QREG && sizeof(E) == 2 && N * DVC / 2 <= 128;
   static constexpr int BN = (PAIR && QRH == 0) ? 32 : FwdTile<E>::BN;
   static constexpr int BM = NW * 32;
-  static constexpr int nQ = QREG ? 0 : (N - QRH) * BM * HS;
-  static constexpr int nK = N * BN * HS;
-  static constexpr int nV = BN * DVC;
+  static constexpr int HSP = img_cols(HS), DVP = img_cols(DVC);     // LDS image widths
+  static constexpr int nQ = QREG ? 0 : (N - QRH) * BM * HSP;
+  static constexpr int nK = N * BN * HSP;
+  static constexpr int nV = BN * DVP;
   static constexpr int NS = ring_stages_lim(nQ * (int)sizeof(E), (nK + nV) * (int)sizeof(E),
                                             PAIR ? 80 * 1024 : 160 * 1024);
   static constexpr int bytes = (nQ + NS * nK + NS * nV) * (int)sizeof(E);
@@ -517,10 +533,11 @@ __global__ __launch_bounds__(NW * 64, (FwdCfg<E, HS, N, DVC, NW, QREG, QRH>::PAI
 void attn_fwd_kernel(FwdParams p) {
   using O = Ops<E>;
   using frag = typename O::frag;
-  using QI = Img<E, HS>;
-  using KI = Img<E, HS>;
-  using VI = Img<E, DVC>;
   using CF = FwdCfg<E, HS, N, DVC, NW, QREG, QRH>;
+  constexpr int HSP = CF::HSP, DVP = CF::DVP;
+  using QI = Img<E, HSP>;
+  using KI = Img<E, HSP>;
+  using VI = Img<E, DVP>;
   constexpr int NQR = QREG ? N : QRH;      // branches whose Q rows live in registers
   constexpr int BN = CF::BN, BM = CF::BM, NTHR = NW * 64;
   constexpr int KS = O::KSTEP;
@@ -533,8 +550,8 @@ void attn_fwd_kernel(FwdParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   E* Qs = reinterpret_cast<E*>(smem);
   constexpr int NS = CF::NS;
-  E* Kb = Qs + CF::nQ;              // [NS][N][BN][HS]  ring
-  E* Vb = Kb + NS * CF::nK;         // [NS][BN][DVC]
+  E* Kb = Qs + CF::nQ;              // [NS][N][BN][HSP]  ring
+  E* Vb = Kb + NS * CF::nK;         // [NS][BN][DVP]
 
   // wave index is wave-uniform: make it provably so (SGPR), or every branch on it
   // becomes an exec-masked divergent branch
@@ -569,7 +586,7 @@ void attn_fwd_kernel(FwdParams p) {
                           : O::zero();
 #pragma unroll
   for (int i = NQR; i < N; ++i)
-    stage<E, HS, BM, HS, NTHR>(Qs + (i - NQR) * BM * HS, gq + i * p.q.si, p.q.st, q0, T - 1, tid);
+    stage<E, HSP, BM, HS, NTHR>(Qs + (i - NQR) * BM * HSP, gq + i * p.q.si, p.q.st, q0, T - 1, tid);
 
   const int kend = min(T, q0 + BM);
   const int ntiles = (kend + BN - 1) / BN;
@@ -582,16 +599,16 @@ void attn_fwd_kernel(FwdParams p) {
   auto stage_kv = [&](int kt, int buf) {
     const int k0 = kt * BN;
     if constexpr (PRE) {
-      KR::issue_pre(gk, p.k.st, gv, p.v.st, k0, T, Kb + buf * N * BN * HS, Vb + buf * BN * DVC, wave, doff);
+      KR::issue_pre(gk, p.k.st, gv, p.v.st, k0, T, Kb + buf * CF::nK, Vb + buf * CF::nV, wave, doff);
     } else {
 #pragma unroll
       for (int i = 0; i < N; ++i)
-        stage<E, HS, BN, HS, NTHR>(Kb + (buf * N + i) * BN * HS, gk + i * p.k.si, p.k.st, k0, T - 1, tid);
-      stage<E, DVC, BN, DVC, NTHR>(Vb + buf * BN * DVC, gv, p.v.st, k0, T - 1, tid);
+        stage<E, HSP, BN, HS, NTHR>(Kb + (buf * N + i) * BN * HSP, gk + i * p.k.si, p.k.st, k0, T - 1, tid);
+      stage<E, DVP, BN, DVC, NTHR>(Vb + buf * CF::nV, gv, p.v.st, k0, T - 1, tid);
     }
   };
   const int tile_pieces = SRD ? KR::pieces(wave)
-                              : N * stage_pieces<E, HS, BN, HS, NW>(wave) + stage_pieces<E, DVC, BN, DVC, NW>(wave);
+                              : N * stage_pieces<E, HSP, BN, HS, NW>(wave) + stage_pieces<E, DVP, BN, DVC, NW>(wave);
   for (int j = 0; j < NS - 1; ++j)
     if (j < ntiles) stage_kv(j, j);
   wait_vm(tile_pieces * max(0, min(NS - 1, ntiles) - 1));   // tile 0 (and the Q block) landed
@@ -686,16 +703,16 @@ void attn_fwd_kernel(FwdParams p) {
     constexpr bool MASK = decltype(MASKED)::value;
     const int buf = kt % NS;
     const int k0 = kt * BN;
-    const E* Kc = Kb + buf * N * BN * HS;
+    const E* Kc = Kb + buf * CF::nK;
     f32x16 sa[N][NKB];
 #pragma unroll
     for (int i = 0; i < N; ++i) {
-      const E* Ki = Kc + i * BN * HS;
+      const E* Ki = Kc + i * BN * HSP;
       if constexpr (sizeof(E) == 2) {
         // row operands: byte R*ROWB + (Lrow ^ 32 s) for a 32-row block at row R
         const int Lr = LrK;
         const char* kbase = reinterpret_cast<const char*>(Ki);
-        const char* qbase = reinterpret_cast<const char*>(Qs + (i >= NQR ? i - NQR : 0) * BM * HS) + wave * 32 * QI::ROWB;
+        const char* qbase = reinterpret_cast<const char*>(Qs + (i >= NQR ? i - NQR : 0) * BM * HSP) + wave * 32 * QI::ROWB;
 #pragma unroll
         for (int kb = 0; kb < NKB; ++kb) sa[i][kb] = f32x16{};
         if constexpr (NSQ * (NKB + 1) <= 12 && QRH == 0) {
@@ -738,7 +755,7 @@ void attn_fwd_kernel(FwdParams p) {
           for (int s = 0; s < NSQ; ++s) {
             frag qb;
             if (i < NQR) qb = qf[i < NQR ? i : 0][s];
-            else qb = QI::row(Qs + (i >= NQR ? i - NQR : 0) * BM * HS, wave * 32 + c32, s, hf);
+            else qb = QI::row(Qs + (i >= NQR ? i - NQR : 0) * BM * HSP, wave * 32 + c32, s, hf);
             sa[i][kb] = O::mma(KI::row(Ki, kb * 32 + c32, s, hf), qb, sa[i][kb]);
           }
         }
@@ -748,7 +765,7 @@ void attn_fwd_kernel(FwdParams p) {
   };
   // O_i^T += V^T P_i^T, one V fragment feeds every branch
   auto phase_b = [&](int kt, const frag (&pf)[N][NKB * SPB]) {
-    const E* Vc = Vb + (kt % NS) * BN * DVC;
+    const E* Vc = Vb + (kt % NS) * CF::nV;
     if constexpr (sizeof(E) == 2) {
       const unsigned vb = lds_addr(Vc);
       const int Lv = LtV;
@@ -846,17 +863,20 @@ void attn_fwd_kernel(FwdParams p) {
 }
 
 // ------------------------------------------------------ backward: dQ ---
-template <class E, int HS, int N, int DV, int NW, bool QREG, int QRH = 0>
+template <class E, int HS, int N, int DV, int NW, bool QREG, int QRH = 0, bool BN32 = false>
 struct DqCfg {
   // QRH > 0 (paired plan): the first QRH branches' Q rows stay in registers, the
   // rest in LDS, so Q plus a 2-stage ring of 64-key tiles fits 80 KB
   static constexpr bool PAIR = NW == 4 && !QREG && sizeof(E) == 2;
-  static constexpr int BN = (PAIR && QRH == 0) ? 32 : FwdTile<E>::BN;
+  // BN32: 32-key tiles where no plan with 64-key tiles fits (N = 4 at head size >= 96)
+  static constexpr int BN = (PAIR && QRH == 0) || BN32 ? 32 : FwdTile<E>::BN;
   static constexpr int BM = NW * 32;
-  static constexpr int HSP = HS < 32 ? 32 : HS;
-  static constexpr int nQ = QREG ? 0 : (N - QRH) * BM * HS;
+  // LDS image widths: K rows at least 32 columns (the transposed reads of dQ = dS K take
+  // 32-column blocks), every row a power-of-two pitch
+  static constexpr int HSP = img_cols(HS < 32 ? 32 : HS), QP = img_cols(HS), DVP = img_cols(DV);
+  static constexpr int nQ = QREG ? 0 : (N - QRH) * BM * QP;
   static constexpr int nK = N * BN * HSP;
-  static constexpr int nV = BN * DV;
+  static constexpr int nV = BN * DVP;
   static constexpr int NS = ring_stages_lim(nQ * (int)sizeof(E), (nK + nV) * (int)sizeof(E),
                                             PAIR ? 80 * 1024 : 160 * 1024);
   static constexpr int bytes = (nQ + NS * nK + NS * nV) * (int)sizeof(E);
@@ -875,30 +895,31 @@ struct DqPick {
   static constexpr int NW = pair ? 4 : (q8 ? 8 : (sizeof(E) == 2 ? 4 : 2));
   static constexpr bool QREG = pair ? false : !q8;
   static constexpr int QH = pair ? QRH : 0;
-  static constexpr bool ok = DqCfg<E, HS, N, DV, NW, QREG, QH>::bytes <= LIM;
+  static constexpr bool B32 = DqCfg<E, HS, N, DV, NW, QREG, QH>::bytes > LIM;   // 32-key tiles (fallback)
+  static constexpr bool ok = DqCfg<E, HS, N, DV, NW, QREG, QH, B32>::bytes <= LIM;
 };
 
-template <class E, int HS, int N, int DV, int NW, bool QREG, bool OUTF32, bool SRD, bool DROP, int QRH>
-__global__ __launch_bounds__(NW * 64, simd_waves(NW, DqCfg<E, HS, N, DV, NW, QREG, QRH>::bytes))
+template <class E, int HS, int N, int DV, int NW, bool QREG, bool OUTF32, bool SRD, bool DROP, int QRH, bool B32>
+__global__ __launch_bounds__(NW * 64, simd_waves(NW, DqCfg<E, HS, N, DV, NW, QREG, QRH, B32>::bytes))
 void attn_dq_kernel(BwdParams p) {
   using O = Ops<E>;
   using frag = typename O::frag;
-  using CF = DqCfg<E, HS, N, DV, NW, QREG, QRH>;
+  using CF = DqCfg<E, HS, N, DV, NW, QREG, QRH, B32>;
   constexpr int NQR = QREG ? N : QRH;      // branches whose Q rows live in registers
-  using QI = Img<E, HS>;
-  constexpr int HSP = CF::HSP;
+  constexpr int HSP = CF::HSP, QP = CF::QP, DVP = CF::DVP;
+  using QI = Img<E, QP>;
   using KI = Img<E, HSP>;
-  using VI = Img<E, DV>;
+  using VI = Img<E, DVP>;
   constexpr int BN = CF::BN, BM = CF::BM, NTHR = NW * 64;
   constexpr int KS = O::KSTEP;
   constexpr int NSQ = HS / KS, NSV = DV / KS;
-  constexpr int NKB = BN / 32, SPB = 32 / KS, NHB = HSP / 32;
+  constexpr int NKB = BN / 32, SPB = 32 / KS, NHB = (HS + 31) / 32;
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  E* Qs = reinterpret_cast<E*>(smem);   // [N][BM][HS] unless QREG
+  E* Qs = reinterpret_cast<E*>(smem);   // [N][BM][QP] unless QREG
   constexpr int NS = CF::NS;
   E* Kb = Qs + CF::nQ;                  // [NS][N][BN][HSP]  ring
-  E* Vb = Kb + NS * CF::nK;             // [NS][BN][DV]
+  E* Vb = Kb + NS * CF::nK;             // [NS][BN][DVP]
 
   // wave index is wave-uniform: make it provably so (SGPR), or every branch on it
   // becomes an exec-masked divergent branch
@@ -924,21 +945,21 @@ void attn_dq_kernel(BwdParams p) {
   const int kend = min(T, q0 + BM);
   const int ntiles = (kend + BN - 1) / BN;
   using KR = KvRing<E, HS, N, DV, BN, NW>;
-  static_assert(!SRD || HSP == HS, "descriptor staging needs unpadded K rows");
+  static_assert(!SRD || (HSP == KR::HSP && DVP == KR::DVP), "descriptor staging fills the kernel's images");
   constexpr bool PRE = SRD && !DROP;  // DMA source offsets computed once (dropout: fewer spills without)
   uint32_t doff[PRE ? KR::MYP : 1];
   if constexpr (PRE) KR::offsets(p.k.st, p.k.si, p.v.st, wave, lane, doff);
   auto stage_kv = [&](int kt, int buf) {
     const int k0 = kt * BN;
     if constexpr (PRE) {
-      KR::issue_pre(gk, p.k.st, gv, p.v.st, k0, T, Kb + buf * N * BN * HSP, Vb + buf * BN * DV, wave, doff);
+      KR::issue_pre(gk, p.k.st, gv, p.v.st, k0, T, Kb + buf * CF::nK, Vb + buf * CF::nV, wave, doff);
     } else if constexpr (SRD) {
-      KR::issue(gk, p.k.st, p.k.si, gv, p.v.st, k0, T, Kb + buf * N * BN * HSP, Vb + buf * BN * DV, wave, lane);
+      KR::issue(gk, p.k.st, p.k.si, gv, p.v.st, k0, T, Kb + buf * CF::nK, Vb + buf * CF::nV, wave, lane);
     } else {
 #pragma unroll
       for (int i = 0; i < N; ++i)
         stage<E, HSP, BN, HS, NTHR>(Kb + (buf * N + i) * BN * HSP, gk + i * p.k.si, p.k.st, k0, T - 1, tid);
-      stage<E, DV, BN, DV, NTHR>(Vb + buf * BN * DV, gv, p.v.st, k0, T - 1, tid);
+      stage<E, DVP, BN, DV, NTHR>(Vb + buf * CF::nV, gv, p.v.st, k0, T - 1, tid);
     }
   };
 
@@ -995,10 +1016,10 @@ void attn_dq_kernel(BwdParams p) {
   if constexpr (!QREG) {
 #pragma unroll
     for (int i = NQR; i < N; ++i)
-      stage<E, HS, BM, HS, NTHR>(Qs + (i - NQR) * BM * HS, gq + i * p.q.si, p.q.st, q0, T - 1, tid);
+      stage<E, QP, BM, HS, NTHR>(Qs + (i - NQR) * BM * QP, gq + i * p.q.si, p.q.st, q0, T - 1, tid);
   }
   const int tile_pieces = SRD ? KR::pieces(wave)
-                              : N * stage_pieces<E, HSP, BN, HS, NW>(wave) + stage_pieces<E, DV, BN, DV, NW>(wave);
+                              : N * stage_pieces<E, HSP, BN, HS, NW>(wave) + stage_pieces<E, DVP, BN, DV, NW>(wave);
   for (int j = 0; j < NS - 1; ++j)
     if (j < ntiles) stage_kv(j, j);
   wait_vm(tile_pieces * max(0, min(NS - 1, ntiles) - 1));
@@ -1043,8 +1064,8 @@ void attn_dq_kernel(BwdParams p) {
     if (kt + NS - 1 < ntiles) stage_kv(kt + NS - 1, (kt + NS - 1) % NS);
     const int k0 = kt * BN;
     if (wave_live && k0 <= qw0 + 31) {
-      const E* Kc = Kb + buf * N * BN * HSP;
-      const E* Vc = Vb + buf * BN * DV;
+      const E* Kc = Kb + buf * CF::nK;
+      const E* Vc = Vb + buf * CF::nV;
       unsigned bV = 0, bK = 0, tK = 0;
       if constexpr (XA) {
         bV = LrV + lds_addr(Vc); bK = LrK + lds_addr(Kc); tK = LtK + lds_addr(Kc);
@@ -1080,7 +1101,7 @@ void attn_dq_kernel(BwdParams p) {
           if constexpr (sizeof(E) == 2) {
             const int Lr = LrK;
             const char* kbase = reinterpret_cast<const char*>(Ki);
-            const char* qbase = reinterpret_cast<const char*>(Qs + (i >= NQR ? i - NQR : 0) * BM * HS) +
+            const char* qbase = reinterpret_cast<const char*>(Qs + (i >= NQR ? i - NQR : 0) * BM * QP) +
                                 wave * 32 * QI::ROWB;
             const int Lq = LrQ;
 #pragma unroll
@@ -1107,7 +1128,7 @@ void attn_dq_kernel(BwdParams p) {
               for (int s = 0; s < NSQ; ++s) {
                 frag qb;
                 if (i < NQR) qb = qf[i < NQR ? i : 0][s];
-                else qb = QI::row(Qs + (i >= NQR ? i - NQR : 0) * BM * HS, wave * 32 + c32, s, hf);
+                else qb = QI::row(Qs + (i >= NQR ? i - NQR : 0) * BM * QP, wave * 32 + c32, s, hf);
                 sa[kb] = O::mma(KI::row(Ki, kb * 32 + c32, s, hf), qb, sa[kb]);
               }
             }
@@ -1189,33 +1210,42 @@ void attn_dq_kernel(BwdParams p) {
 
 // One query tile of the key-major backward -- Q_i rows, dO rows, LSE rows and
 // (with DELTA) c*delta rows -- streamed into one ring stage by buffer_load ... lds.
-// Stage layout: [N][BQ][HS] Q image | [BQ][DV] dO image | [NP] lse | [NP] c*delta.
+// Stage layout: [N][BQ][HSP] Q image | [BQ][DVP] dO image | [NP] lse | [NP] c*delta
+// (image widths padded to a power of two, img_cols).
 // Every per-lane source offset is computed once (init); a tile then costs only
 // scalar descriptor setup.  Rows past T read as zeros (and are masked).
-template <class E, int HS, int N, int DV, int NW, bool DELTA, int BQ_ = 32>
+template <class E, int HS, int N, int DV, int NW, bool DELTA, int BQ_ = 32, bool ROWS = true>
 struct TileRing {
   static constexpr int ES = (int)sizeof(E), BQ = BQ_;
   static constexpr int NP = (N * BQ + 63) / 64 * 64;
-  static constexpr int QB = BQ * HS * ES, DB = BQ * DV * ES;
-  static constexpr int OFF_D = N * QB, OFF_L = OFF_D + DB, OFF_G = OFF_L + NP * 4, SB = OFF_G + NP * 4;
+  static constexpr int HSP = img_cols(HS), DVP = img_cols(DV);
+  static constexpr int QB = BQ * HSP * ES, DB = BQ * DVP * ES;
+  // ROWS = false: the LSE / delta row vectors are not staged (read from global memory)
+  static constexpr int OFF_D = N * QB, OFF_L = OFF_D + DB, OFF_G = OFF_L + NP * 4;
+  static constexpr int SB = ROWS ? OFF_G + NP * 4 : OFF_L;
   static constexpr int PQ = N * QB / 1024, PD = DB / 1024, PL = NP / 64;
-  static constexpr int NPC = PQ + PD + (DELTA ? 2 : 1) * PL;     // DMA pieces per stage
+  static constexpr int NPC = PQ + PD + (ROWS ? (DELTA ? 2 : 1) * PL : 0);     // DMA pieces per stage
   static constexpr int MYP = (NPC + NW - 1) / NW;                  // piece j goes to wave j % NW
   static constexpr bool ok = ES == 2 && HS >= 32 && QB % 1024 == 0 && DB % 1024 == 0;
 
   __device__ static int pieces(int wave) { return NPC / NW + (wave < NPC % NW ? 1 : 0); }
 
   // byte offset of lane's 16 (or 4) bytes of piece j from the tile's row base
+  // (pad chunks of a padded image read the row's first chunk: in bounds, never used)
   __device__ static uint32_t offq(const BwdParams& p, int j, int lane) {           // j < PQ
-    using QI = Img<E, HS>;
+    using QI = Img<E, HSP>;
     const int i = j / (QB / 1024), pb = (j % (QB / 1024)) * 1024 + lane * 16;
-    const int r = pb / QI::ROWB, c = ((pb % QI::ROWB) >> 4) ^ swz<QI::ROWB>(r);
+    const int r = pb / QI::ROWB;
+    int c = ((pb % QI::ROWB) >> 4) ^ swz<QI::ROWB>(r);
+    if constexpr (HSP != HS) c = c * 16 < HS * ES ? c : 0;
     return (uint32_t)(r * (uint32_t)(p.q.st * ES) + (uint32_t)(i * p.q.si * ES) + c * 16);
   }
   __device__ static uint32_t offd(const BwdParams& p, int j, int lane) {           // PQ <= j < PQ + PD
-    using DI = Img<E, DV>;
+    using DI = Img<E, DVP>;
     const int pb = (j - PQ) * 1024 + lane * 16;
-    const int r = pb / DI::ROWB, c = ((pb % DI::ROWB) >> 4) ^ swz<DI::ROWB>(r);
+    const int r = pb / DI::ROWB;
+    int c = ((pb % DI::ROWB) >> 4) ^ swz<DI::ROWB>(r);
+    if constexpr (DVP != DV) c = c * 16 < DV * ES ? c : 0;
     return (uint32_t)(r * (uint32_t)(p.dout.st * ES) + c * 16);
   }
   __device__ static uint32_t offr(int j, int lane, int64_t bstride) {              // row-vector pieces
@@ -1274,26 +1304,32 @@ inline bool ring_layout_ok(const BwdParams& p, int es) {
 
 // --------------------------------------------------- backward: dK, dV ---
 
-template <class E, int HS, int N, int DV, int NW, bool PR = false>
+template <class E, int HS, int N, int DV, int NW, bool PR = false, bool GRX = false>
 struct DkdvCfg {
   static constexpr int LIMB = PR ? 80 * 1024 : 160 * 1024;     // PR: paired 4-wave plan, two per CU
   static constexpr int BK = NW * 32;
-  static constexpr int HSP = HS < 32 ? 32 : HS;
+  // LDS image widths (img_cols): Q rows at least 32 columns (dK's transposed reads take
+  // 32-column blocks); K (row reads only) and dO at their power-of-two pitch
+  static constexpr int HSP = img_cols(HS < 32 ? 32 : HS), KP = img_cols(HS), DVP = img_cols(DV);
   static constexpr int BQ = 32;                            // query rows per ring stage
   static constexpr int NP = (N * BQ + 63) / 64 * 64;      // fp32 row vectors, padded to DMA pieces
   static constexpr int nQ = N * BQ * HSP;
-  static constexpr int nD = BQ * DV;
-  static constexpr int nK = N * BK * HS;                   // the workgroup's K_i rows (B of S_i)
-  static constexpr int NS = ring_stages_lim(nK * (int)sizeof(E), (nQ + nD) * (int)sizeof(E) + 2 * NP * 4, LIMB);
-  static constexpr int bytes = (nK + NS * nQ + NS * nD) * (int)sizeof(E) + NS * 2 * NP * 4;
+  static constexpr int nD = BQ * DVP;
+  static constexpr int nK = N * BK * KP;                   // the workgroup's K_i rows (B of S_i)
+  // GR (DkdvWaves sets it where no plan fits otherwise: N = 4 at head size >= 96, fp32
+  // N = 4): the LSE / delta row vectors are read from global memory instead of the ring
+  static constexpr int RB = 2 * NP * 4;                    // row-vector bytes per stage
+  static constexpr bool GR = GRX;
+  static constexpr int NS = ring_stages_lim(nK * (int)sizeof(E), (nQ + nD) * (int)sizeof(E) + (GR ? 0 : RB), LIMB);
+  static constexpr int bytes = (nK + NS * nQ + NS * nD) * (int)sizeof(E) + (GR ? 0 : NS * RB);
 };
 
 // widest key block (waves x 32 keys) whose K rows plus a 2+-stage query ring fit LDS
 // accumulator budget -> whether dK and dV share one launch
 template <int HS, int N, int DV>
 struct DkdvSplit {
-  static constexpr int HSP = HS < 32 ? 32 : HS;
-  static constexpr bool fused = (N * HSP / 2 + DV / 2) <= 160;
+  static constexpr int HSB = (HS < 32 ? 32 : HS + 31) / 32 * 32;     // dK accumulator columns
+  static constexpr bool fused = (N * HSB / 2 + DV / 2) <= 160;
 };
 
 // widest key block (waves x 32 keys) whose K rows plus a 2+-stage query ring fit
@@ -1302,43 +1338,50 @@ struct DkdvSplit {
 template <class E, int HS, int N, int DV, bool NP = false>
 struct DkdvWaves {
   static constexpr int LIM = 160 * 1024;
-  static constexpr int HSP = HS < 32 ? 32 : HS;
-  static constexpr int regs8 = DkdvSplit<HS, N, DV>::fused ? N * HSP / 2 + DV / 2 + DV / 4 + 88
-                             : (N * HSP / 2 + DV / 4 > DV / 2 ? N * HSP / 2 + DV / 4 : DV / 2) + 88;
+  static constexpr int HSB = DkdvSplit<HS, N, DV>::HSB;
+  static constexpr int regs8 = DkdvSplit<HS, N, DV>::fused ? N * HSB / 2 + DV / 2 + DV / 4 + 88
+                             : (N * HSB / 2 + DV / 4 > DV / 2 ? N * HSB / 2 + DV / 4 : DV / 2) + 88;
   static constexpr int v8 = (sizeof(E) == 2 && DkdvCfg<E, HS, N, DV, 8>::bytes <= LIM && regs8 <= 256) ? 8
                           : DkdvCfg<E, HS, N, DV, 4>::bytes <= LIM ? 4 : 2;
   // paired plan: where the 8-wave plan applies, two 4-wave workgroups per CU instead
   // (bf16 only: the fp16 paired instantiation spills 16 VGPRs)
   static constexpr bool pair = !NP && std::is_same<E, __bf16>::value && v8 == 8 &&
                                DkdvCfg<E, HS, N, DV, 4, true>::bytes <= 80 * 1024;
-  static constexpr int v = pair ? 4 : v8;
+  static constexpr int v0 = pair ? 4 : v8;
+  // no plan with the row vectors in the ring fits: two waves (one where two do not fit:
+  // fp32 at head size 96), row vectors from global memory
+  static constexpr bool gr = DkdvCfg<E, HS, N, DV, v0, pair>::bytes > LIM;
+  static constexpr int v = !gr ? v0 : (DkdvCfg<E, HS, N, DV, 2, false, true>::bytes <= LIM ? 2 : 1);
 };
 
-template <class E, int HS, int N, int DV, int NW, bool DK, bool DVV, bool SRD, bool DROP, bool PR>
+template <class E, int HS, int N, int DV, int NW, bool DK, bool DVV, bool SRD, bool DROP, bool PR, bool GRX>
 __global__ __launch_bounds__(NW * 64, (NW >= 8 || PR ? 2 : 1))
 void attn_dkdv_kernel(BwdParams p) {
   using O = Ops<E>;
   using frag = typename O::frag;
-  using CF = DkdvCfg<E, HS, N, DV, NW, PR>;
-  constexpr int HSP = CF::HSP, BQ = CF::BQ, BK = CF::BK, NP = CF::NP, NTHR = NW * 64;
+  using CF = DkdvCfg<E, HS, N, DV, NW, PR, GRX>;
+  constexpr int HSP = CF::HSP, KP = CF::KP, DVP = CF::DVP, BQ = CF::BQ, BK = CF::BK, NP = CF::NP;
+  constexpr int NTHR = NW * 64;
   using QI = Img<E, HSP>;
-  using DI = Img<E, DV>;
+  using DI = Img<E, DVP>;
   constexpr int KS = O::KSTEP;
   constexpr int NSQ = HS / KS, NSV = DV / KS, SPB = 32 / KS;
-  constexpr int NHB = HSP / 32, NVB = DV / 32;
+  constexpr int NHB = (HS + 31) / 32, NVB = DV / 32;
 
-  using KI = Img<E, HS>;
+  using KI = Img<E, KP>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  E* Ks = reinterpret_cast<E*>(smem);     // [N][BK][HS]
-  E* Qb = Ks + CF::nK;                    // [2][N][BQ][HSP]
+  E* Ks = reinterpret_cast<E*>(smem);     // [N][BK][KP]
+  E* Qb = Ks + CF::nK;                    // [NS][N][BQ][HSP]
   constexpr int NS = CF::NS;
-  E* Db = Qb + NS * CF::nQ;               // [NS][BQ][DV]
+  E* Db = Qb + NS * CF::nQ;               // [NS][BQ][DVP]
   float* Lb = reinterpret_cast<float*>(Db + NS * CF::nD);  // [NS][NP] lse
   float* Gb = Lb + NS * NP;                                 // [NS][NP] delta
   // SRD: the ring is instead NS stages of TileRing's layout, filled by buffer_load ... lds
-  using RG = TileRing<E, HS, N, DV, NW, DK, BQ>;
+  constexpr bool GR = CF::GR;
+  using RG = TileRing<E, HS, N, DV, NW, DK, BQ, !GR>;
   char* ringb = reinterpret_cast<char*>(Qb);
-  static_assert(!SRD || (RG::ok && RG::SB * NS <= CF::bytes - CF::nK * (int)sizeof(E)), "ring layout");
+  static_assert(!SRD || (RG::ok && RG::SB * NS <= CF::bytes - CF::nK * (int)sizeof(E) && RG::HSP == HSP &&
+                          RG::DVP == DVP), "ring layout");
 
   // wave index is wave-uniform: make it provably so (SGPR), or every branch on it
   // becomes an exec-masked divergent branch
@@ -1387,9 +1430,11 @@ void attn_dkdv_kernel(BwdParams p) {
 #pragma unroll
       for (int i = 0; i < N; ++i)
         stage<E, HSP, BQ, HS, NTHR>(Qb + (buf * N + i) * BQ * HSP, gq + i * p.q.si, p.q.st, q0, T - 1, tid);
-      stage<E, DV, BQ, DV, NTHR>(Db + buf * BQ * DV, gdo, p.dout.st, q0, T - 1, tid);
-      stage_rows<N, BQ, NTHR>(Lb + buf * NP, p.lse + rowvec, bstride, q0, T - 1, tid);
-      if constexpr (DK) stage_rows<N, BQ, NTHR>(Gb + buf * NP, p.delta + rowvec, bstride, q0, T - 1, tid);
+      stage<E, DVP, BQ, DV, NTHR>(Db + buf * CF::nD, gdo, p.dout.st, q0, T - 1, tid);
+      if constexpr (!GR) {
+        stage_rows<N, BQ, NTHR>(Lb + buf * NP, p.lse + rowvec, bstride, q0, T - 1, tid);
+        if constexpr (DK) stage_rows<N, BQ, NTHR>(Gb + buf * NP, p.delta + rowvec, bstride, q0, T - 1, tid);
+      }
     }
   };
 
@@ -1404,9 +1449,9 @@ void attn_dkdv_kernel(BwdParams p) {
 
   const int ntiles = kb0 < T ? (T - kb0 + BQ - 1) / BQ : 0;
 #pragma unroll
-  for (int i = 0; i < N; ++i) stage<E, HS, BK, HS, NTHR>(Ks + i * BK * HS, gk + i * p.k.si, p.k.st, kb0, T - 1, tid);
+  for (int i = 0; i < N; ++i) stage<E, KP, BK, HS, NTHR>(Ks + i * BK * KP, gk + i * p.k.si, p.k.st, kb0, T - 1, tid);
   const int tile_pieces = SRD ? RG::pieces(wave)
-                              : N * stage_pieces<E, HSP, BQ, HS, NW>(wave) + stage_pieces<E, DV, BQ, DV, NW>(wave) +
+                              : N * stage_pieces<E, HSP, BQ, HS, NW>(wave) + stage_pieces<E, DVP, BQ, DV, NW>(wave) +
                                     rows_pieces<N, BQ, NW>(wave) * (DK ? 2 : 1);
   for (int j = 0; j < NS - 1; ++j)
     if (j < ntiles) stage_q(kb0 + j * BQ, j);
@@ -1456,9 +1501,20 @@ void attn_dkdv_kernel(BwdParams p) {
     if (wave_keys && q0 + 31 >= kw0) {
       const char* sg = ringb + buf * RG::SB;
       const E* Qc = SRD ? reinterpret_cast<const E*>(sg) : Qb + buf * N * BQ * HSP;
-      const E* Dc = SRD ? reinterpret_cast<const E*>(sg + RG::OFF_D) : Db + buf * BQ * DV;
+      const E* Dc = SRD ? reinterpret_cast<const E*>(sg + RG::OFF_D) : Db + buf * CF::nD;
       const float* Lc = SRD ? reinterpret_cast<const float*>(sg + RG::OFF_L) : Lb + buf * NP;
       const float* Gc = SRD ? reinterpret_cast<const float*>(sg + RG::OFF_G) : Gb + buf * NP;
+      // rows 8g + 4hf .. + 3 of branch i's LSE / delta vector: from the ring, or (GR) from
+      // global memory, rows past T clamped (they are masked)
+      auto rows4 = [&](const float* ring, const float* glb, int i, int g) -> f32x4 {
+        if constexpr (GR) {
+          const float* v = glb + rowvec + i * bstride;
+          const int r0 = q0 + 8 * g + 4 * hf;
+          return f32x4{v[min(r0, T - 1)], v[min(r0 + 1, T - 1)], v[min(r0 + 2, T - 1)], v[min(r0 + 3, T - 1)]};
+        } else {
+          return *reinterpret_cast<const f32x4*>(ring + i * BQ + 8 * g + 4 * hf);
+        }
+      };
       unsigned bQ = 0, bD = 0, tQ = 0, tD = 0;
       if constexpr (XA) {
         const unsigned sb = lds_addr(sg);
@@ -1472,7 +1528,7 @@ void attn_dkdv_kernel(BwdParams p) {
       if constexpr (DK && !DROP) {
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          const f32x4 g4 = *reinterpret_cast<const f32x4*>(Gc + 8 * g + 4 * hf);
+          const f32x4 g4 = rows4(Gc, p.delta, 0, g);
 #pragma unroll
           for (int j = 0; j < 4; ++j) dpa[4 * g + j] = g4[j];
         }
@@ -1502,7 +1558,7 @@ void attn_dkdv_kernel(BwdParams p) {
         f32x16 sa;
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          const f32x4 l4 = *reinterpret_cast<const f32x4*>(Lc + i * BQ + 8 * g + 4 * hf);
+          const f32x4 l4 = rows4(Lc, p.lse, i, g);
 #pragma unroll
           for (int j = 0; j < 4; ++j) sa[4 * g + j] = l4[j];
         }
@@ -1510,7 +1566,7 @@ void attn_dkdv_kernel(BwdParams p) {
         if constexpr (sizeof(E) == 2) {
           const int Lq = LrQ, Lk = LrK;
           const char* qbase = reinterpret_cast<const char*>(Qi);
-          const char* kbase = reinterpret_cast<const char*>(Ks + i * BK * HS) + wave * 32 * KI::ROWB;
+          const char* kbase = reinterpret_cast<const char*>(Ks + i * BK * KP) + wave * 32 * KI::ROWB;
           // operand reads of this branch's S ahead of its MFMA chain (see attn_fwd_kernel)
           frag qfr[NSQ], kfr[NSQ];
 #pragma unroll
@@ -1526,13 +1582,13 @@ void attn_dkdv_kernel(BwdParams p) {
         } else {
 #pragma unroll
           for (int s = 0; s < NSQ; ++s)
-            sa = O::mma(QI::row(Qi, c32, s, hf), KI::row(Ks + i * BK * HS, wave * 32 + c32, s, hf), sa);
+            sa = O::mma(QI::row(Qi, c32, s, hf), KI::row(Ks + i * BK * KP, wave * 32 + c32, s, hf), sa);
         }
         // sa[r] = S'_i[q0 + rowof(r)][krow] - LSE; rows 4g..4g+3 of a lane are consecutive
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           f32x4 d4 = f32x4{};
-          if constexpr (DK) if (DROP || i > 0) d4 = *reinterpret_cast<const f32x4*>(Gc + i * BQ + 8 * g + 4 * hf);
+          if constexpr (DK) if (DROP || i > 0) d4 = rows4(Gc, p.delta, i, g);
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const int r = 4 * g + j;
@@ -1669,8 +1725,9 @@ struct Plan {
   using FP = FwdPick<E, HS, N, DV>;
   using DP = DqPick<E, HS, N, DV>;
   static constexpr int KVW = DkdvWaves<E, HS, N, DV>::v;
-  static constexpr bool KPR = DkdvWaves<E, HS, N, DV>::pair;
-  static constexpr bool ok = FP::ok && DP::ok && DkdvCfg<E, HS, N, DV, KVW, KPR>::bytes <= 160 * 1024;
+  static constexpr bool KPR = DkdvWaves<E, HS, N, DV>::pair && !DkdvWaves<E, HS, N, DV>::gr;
+  static constexpr bool ok = FP::ok && DP::ok &&
+                             DkdvCfg<E, HS, N, DV, KVW, KPR, DkdvWaves<E, HS, N, DV>::gr>::bytes <= 160 * 1024;
 };
 
 template <class E, int HS, int N, int DV_, bool DROP>
@@ -1703,17 +1760,19 @@ int launch_dq_t(const BwdParams& p, hipStream_t st) {
   constexpr int NW = DP::NW, DV = PL::DV;
   constexpr bool QR = DP::QREG;
   constexpr int QH = DP::QH;
-  constexpr int bytes = DqCfg<E, HS, N, DV, NW, QR, QH>::bytes;
+  constexpr bool B32 = DP::B32;
+  using CF = DqCfg<E, HS, N, DV, NW, QR, QH, B32>;
+  constexpr int bytes = CF::bytes;
   dim3 grid((p.T + NW * 32 - 1) / (NW * 32), p.H, p.B);
   auto run = [&](auto F32, auto SRDV) -> int {
-    auto kern = attn_dq_kernel<E, HS, N, DV, NW, QR, decltype(F32)::value, decltype(SRDV)::value, DROP, QH>;
+    auto kern = attn_dq_kernel<E, HS, N, DV, NW, QR, decltype(F32)::value, decltype(SRDV)::value, DROP, QH, B32>;
     if (int e = set_smem(kern, bytes)) return e;
     hipLaunchKernelGGL(kern, grid, dim3(NW * 64), bytes, st, p);
     return 0;
   };
   auto go = [&](auto SRDV) -> int { return p.dq32 ? run(std::true_type{}, SRDV) : run(std::false_type{}, SRDV); };
   int e = 0;
-  if constexpr (KvRing<E, HS, N, DV, DqCfg<E, HS, N, DV, NW, QR, QH>::BN, NW>::ok && DqCfg<E, HS, N, DV, NW, QR, QH>::HSP == HS)
+  if constexpr (KvRing<E, HS, N, DV, CF::BN, NW>::ok && CF::HSP == img_cols(HS))
     e = kv_layout_ok(p, (int)sizeof(E)) ? go(std::true_type{}) : go(std::false_type{});
   else
     e = go(std::false_type{});
@@ -1726,14 +1785,16 @@ int launch_dkdv_t(const BwdParams& p, hipStream_t st) {
   using PL = Plan<E, HS, N, DV_>;
   using KW = DkdvWaves<E, HS, N, PL::DV, DROP>;
   constexpr int NW = KW::v, DV = PL::DV;
-  constexpr bool PR = KW::pair;
-  constexpr int bytes = DkdvCfg<E, HS, N, DV, NW, PR>::bytes;
+  constexpr bool GR = KW::gr;
+  constexpr bool PR = KW::pair && !GR;
+  using CF = DkdvCfg<E, HS, N, DV, NW, PR, GR>;
+  constexpr int bytes = CF::bytes;
   dim3 grid((p.T + NW * 32 - 1) / (NW * 32), p.H, p.B);
   dim3 block(NW * 64);
   constexpr bool FUSED = DkdvSplit<HS, N, DV>::fused;
   auto run = [&](auto DKV, auto DVVV, auto SRDV) -> int {
     auto kern = attn_dkdv_kernel<E, HS, N, DV, NW, decltype(DKV)::value, decltype(DVVV)::value, decltype(SRDV)::value,
-                                 DROP, PR>;
+                                 DROP, PR, GR>;
     if (int e = set_smem(kern, bytes)) return e;
     hipLaunchKernelGGL(kern, grid, block, bytes, st, p);
     return 0;
@@ -1747,7 +1808,7 @@ int launch_dkdv_t(const BwdParams& p, hipStream_t st) {
     }
   };
   int e = 0;
-  if constexpr (TileRing<E, HS, N, DV, NW, true, DkdvCfg<E, HS, N, DV, NW, PR>::BQ>::ok) {
+  if constexpr (TileRing<E, HS, N, DV, NW, true, CF::BQ, !GR>::ok) {
     e = ring_layout_ok(p, (int)sizeof(E)) ? go(std::true_type{}) : go(std::false_type{});
   } else {
     e = go(std::false_type{});
@@ -1757,11 +1818,14 @@ int launch_dkdv_t(const BwdParams& p, hipStream_t st) {
 }
 
 // (head size, branches, value width): the differential models' dv = 2 hs, plus the
-// control model's standard attention (N = 1, dv = hs; control.py:38-63)
+// control model's standard attention (N = 1, dv = hs; control.py:38-63).  Head size 96
+// is the reference's own TrainingConfig (n_embd 768, n_head 4: train.py:60-61 with
+// diff_transformer.py:111 gives 768 // 8; the control model's 2 * n_head heads also 96).
 #define DTA_FOR_CONFIGS(X) \
   X(16, 1, 32) X(16, 2, 32) X(16, 3, 32) X(16, 4, 32) X(32, 1, 64) X(32, 2, 64) X(32, 3, 64) X(32, 4, 64) \
   X(64, 1, 128) X(64, 2, 128) X(64, 3, 128) X(64, 4, 128) X(128, 1, 256) X(128, 2, 256) X(128, 3, 256) \
-  X(128, 4, 256) X(64, 1, 64) X(128, 1, 128)
+  X(128, 4, 256) X(64, 1, 64) X(128, 1, 128) \
+  X(96, 1, 192) X(96, 2, 192) X(96, 3, 192) X(96, 4, 192) X(96, 1, 96)
 
 template <class E, bool DROP>
 int dispatch_fwd(const FwdParams& p, hipStream_t st) {

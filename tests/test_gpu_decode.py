@@ -53,7 +53,8 @@ def _decode_case(B, H, N, hs, dv, L, cap, dtype, seed):
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("N,hs,dv", [(1, 64, 64), (2, 32, 64), (2, 64, 128), (3, 64, 128), (4, 32, 64),
                                      (2, 128, 256), (1, 128, 128),
-                                     (2, 48, 96), (1, 32, 32)])     # last two: single-pass plan
+                                     (2, 48, 96), (1, 32, 32),      # single-pass plan
+                                     (2, 96, 192), (4, 96, 192), (1, 96, 96)])   # the reference's default head size
 def test_decode_kernel_matches_oracle(dtype, N, hs, dv):
     for L, cap in [(1, 1), (5, 9), (257, 300), (1000, 1024)]:
         got, want = _decode_case(2, 3, N, hs, dv, L, cap, dtype, seed=L + 7 * N + hs)

@@ -58,6 +58,10 @@ CASES = [  # H, N, hs, T, rope
     (2, 2, 64, 1, False), (1, 2, 64, 256, True),
     # long enough for the K/V ring to wrap many times under the staggered schedule
     (1, 2, 64, 1100, False), (1, 1, 64, 777, False), (1, 3, 32, 1500, True),
+    # head size 96 (the reference's default TrainingConfig: train.py:60-61, diff_transformer.py:111),
+    # N = 4 at head sizes 96 / 128 (dQ 32-key tiles, dK/dV row vectors from global memory)
+    (2, 2, 96, 129, False), (1, 1, 96, 200, False), (1, 3, 96, 70, True), (1, 4, 96, 100, True),
+    (1, 4, 128, 97, False), (1, 2, 96, 700, True),
 ]
 
 

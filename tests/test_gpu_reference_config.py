@@ -1,0 +1,160 @@
+"""The reference's own default configuration on the GPU.
+
+train.py's TrainingConfig is n_embd=768, n_head=4 (train.py:60-61); DiffTransformer and
+AlternatingDiffTransformer (train.py:205-221) then have head_size = 768 // (2 * 4) = 96
+(diff_transformer.py:111) and value width 192, and the live control model
+(StandardTransformer with n_head * 2 = 8 heads, train.py:223-230) has head size 96 too.
+These shapes run on the head-size-96 kernel plans (LDS images padded to 128 / 256
+columns).  The checker is the CPU oracle (fp64) restating the reference model op for op.
+Tolerance (north_star): fp32 max|a-b|/max|b| <= 1e-4, bf16 autocast <= 2e-2.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import rel_err
+from oracle import diffattn_oracle as orc
+
+from differential_transformer_replication_amd import control as C
+from differential_transformer_replication_amd import diff_transformer as D
+from differential_transformer_replication_amd import Ndiff_transformer as ND
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _randomise_lambdas(m, seed=3):
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():                      # off the zero-init saddle (SURVEY semantic 4)
+        for n, p in m.named_parameters():
+            if "lambda_" in n:
+                p.copy_(torch.randn(p.shape, generator=g) * 0.1)
+
+
+def _oracle_diff_transformer(sd, idx, tgt, n_head, n_layer, block):
+    """DiffTransformer.forward (diff_transformer.py:154-175) with Block.forward (:123-126)
+    and SwiGLU (:95-105), on the oracle's MultiHeadDiffAttention restatement."""
+    B, T = idx.shape
+    C_ = sd["ln_f.weight"].shape[0]
+    x = sd["token_embedding_table.weight"][idx] + sd["position_embedding_table.weight"][:T]
+    for i in range(n_layer):
+        p = f"blocks.{i}."
+        h = F.layer_norm(x, (C_,), sd[p + "ln1.weight"], sd[p + "ln1.bias"], 1e-5)
+        x = x + orc.multihead_diff_attention(h, sd, n_head, i + 1, block, prefix=p + "diff_attn.")
+        h = F.layer_norm(x, (C_,), sd[p + "ln2.weight"], sd[p + "ln2.bias"], 1e-5)
+        gate = F.silu(F.linear(h, sd[p + "ffwd.0.linear_gate.weight"], sd[p + "ffwd.0.linear_gate.bias"]))
+        xf = F.linear(h, sd[p + "ffwd.0.linear_xform.weight"], sd[p + "ffwd.0.linear_xform.bias"])
+        x = x + F.linear(gate * xf, sd[p + "ffwd.1.weight"], sd[p + "ffwd.1.bias"])
+    x = F.layer_norm(x, (C_,), sd["ln_f.weight"], sd["ln_f.bias"], 1e-5)
+    logits = F.linear(x, sd["lm_head.weight"], sd["lm_head.bias"])
+    V = logits.shape[-1]
+    return logits.view(B * T, V), F.cross_entropy(logits.view(B * T, V), tgt.view(B * T))
+
+
+def test_default_config_diff_transformer_step_fp32():
+    """DiffTransformer(12000, 768, 4, 2, 512, 0.0): one forward + backward, fp32, logits,
+    loss and EVERY parameter gradient against the fp64 oracle model."""
+    torch.manual_seed(0)
+    m = D.DiffTransformer(12000, 768, 4, 2, 512, 0.0)
+    _randomise_lambdas(m)
+    sd = {k: v.double().requires_grad_(True) for k, v in m.state_dict().items()
+          if v.is_floating_point() and not k.endswith("tril") and not k.endswith("lambda_init")}
+    g = torch.Generator().manual_seed(1)
+    idx = torch.randint(0, 12000, (2, 200), generator=g)
+    tgt = torch.randint(0, 12000, (2, 200), generator=g)
+    ref_logits, ref_loss = _oracle_diff_transformer(sd, idx, tgt, 4, 2, 512)
+    ref_loss.backward()
+    m = m.to(DEV)
+    logits, loss = m(idx.to(DEV), tgt.to(DEV))
+    loss.backward()
+    torch.cuda.synchronize()
+    assert rel_err(logits.float().cpu(), ref_logits.detach()) < 1e-4
+    assert abs(float(loss) - float(ref_loss)) < 1e-4 * abs(float(ref_loss))
+    for n, p in m.named_parameters():
+        want = sd[n].grad
+        assert p.grad is not None, n
+        if float(want.abs().max()) == 0.0:
+            assert float(p.grad.abs().max()) < 1e-8, n
+        else:
+            assert rel_err(p.grad.double().cpu(), want) < 1e-4, (n, rel_err(p.grad.double().cpu(), want))
+
+
+def test_default_config_diff_transformer_bf16_autocast():
+    """The same model under bf16 autocast (the dtype the benchmarks run): logits and the
+    attention parameters' gradients within 2e-2 of the fp64 oracle."""
+    torch.manual_seed(0)
+    m = D.DiffTransformer(12000, 768, 4, 2, 512, 0.0)
+    _randomise_lambdas(m)
+    sd = {k: v.double().requires_grad_(True) for k, v in m.state_dict().items()
+          if v.is_floating_point() and not k.endswith("tril") and not k.endswith("lambda_init")}
+    g = torch.Generator().manual_seed(2)
+    idx = torch.randint(0, 12000, (2, 512), generator=g)
+    tgt = torch.randint(0, 12000, (2, 512), generator=g)
+    ref_logits, ref_loss = _oracle_diff_transformer(sd, idx, tgt, 4, 2, 512)
+    ref_loss.backward()
+    m = m.to(DEV)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        logits, loss = m(idx.to(DEV), tgt.to(DEV))
+    loss.backward()
+    torch.cuda.synchronize()
+    assert rel_err(logits.float().cpu(), ref_logits.detach()) < 2e-2
+    for n, p in m.named_parameters():
+        if ".diff_attn." in n and "lambda_" not in n:        # lambda bars: test_gpu_modules BF16_LOOSE
+            assert rel_err(p.grad.double().cpu(), sd[n].grad) < 2e-2, (n, rel_err(p.grad.double().cpu(), sd[n].grad))
+
+
+@pytest.mark.parametrize("n_terms", [2, 3, 4])
+def test_default_config_alternating_attention_bf16(n_terms):
+    """MultiHeadAlternatingDiffAttention(4, 96, 768, 0, 512, n_terms) -- the N-diff model at
+    the default config (RoPE on every Q_i / K_i) -- under bf16 autocast: output, input
+    gradient and projection-weight gradients against the fp64 oracle."""
+    torch.manual_seed(n_terms)
+    m = ND.MultiHeadAlternatingDiffAttention(4, 96, 768, 0.0, 512, n_terms)
+    _randomise_lambdas(m, seed=n_terms)
+    full = m.state_dict()
+    sd = {k: (v.double().requires_grad_(True) if v.is_floating_point() else v) for k, v in full.items()
+          if not k.endswith("tril") and not k.endswith("lambda_init")}
+    g = torch.Generator().manual_seed(10 + n_terms)
+    x = torch.randn(2, 300, 768, generator=g)
+    gout = torch.randn(2, 300, 768, generator=g)
+    x64 = x.double().requires_grad_(True)
+    ref = orc.multihead_alternating_diff_attention(x64, sd, 4, n_terms, 3, 512)
+    (ref * gout.double()).sum().backward()
+    m = m.to(DEV)
+    xg = x.to(DEV).requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        out = m(xg, 3)
+    (out.float() * gout.to(DEV)).sum().backward()
+    torch.cuda.synchronize()
+    assert rel_err(out.float().cpu(), ref.detach()) < 2e-2
+    assert rel_err(xg.grad.cpu(), x64.grad) < 2e-2
+    for n, p in m.named_parameters():
+        if n.endswith(".weight") and (".queries." in n or ".keys." in n or ".value." in n or n.startswith("proj")):
+            assert rel_err(p.grad.double().cpu(), sd[n].grad) < 2e-2, (n, rel_err(p.grad.double().cpu(), sd[n].grad))
+
+
+def test_default_config_control_attention_fp32():
+    """control.py's MultiHeadAttention at the live train.py model's shape: 8 heads of
+    head size 96 (dv = hs) on the fused N=1 kernels, fp32, against the oracle."""
+    from differential_transformer_replication_amd import ops
+    assert ops.supported(torch.float32, 96, 1, 96)      # the fused path, not torch's SDPA
+    torch.manual_seed(0)
+    m = C.MultiHeadAttention(8, 96, 768, 0.0, 512)
+    full = m.state_dict()
+    sd = {k: (v.double().requires_grad_(True) if v.is_floating_point() else v) for k, v in full.items()
+          if not k.endswith("tril")}
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(2, 257, 768, generator=g)
+    gout = torch.randn(2, 257, 768, generator=g)
+    x64 = x.double().requires_grad_(True)
+    ref = orc.control_multihead(x64, sd, 8, 512)
+    (ref * gout.double()).sum().backward()
+    m = m.to(DEV)
+    xg = x.to(DEV).requires_grad_(True)
+    out = m(xg)
+    (out * gout.to(DEV)).sum().backward()
+    torch.cuda.synchronize()
+    assert rel_err(out.cpu(), ref.detach()) < 1e-4
+    assert rel_err(xg.grad.cpu(), x64.grad) < 1e-4
+    for n, p in m.named_parameters():
+        assert rel_err(p.grad.double().cpu(), sd[n].grad) < 1e-4, n
