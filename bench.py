@@ -346,7 +346,7 @@ def configs_leg(args):
     out = {}
     for n in (3, 4):
         torch.cuda.empty_cache()
-        r = train_bench(argparse.Namespace(steps=args.cfg_steps, warmup=2, model="ndiff", n_terms=n,
+        r = train_bench(argparse.Namespace(steps=args.cfg_steps, warmup=3, model="ndiff", n_terms=n,
                                            device="cuda"), 1, 0)
         torch.cuda.empty_cache()
         sec, flop, kernels = core_run(16, 6, 64, n, 2048, args.cfg_steps, 2)
@@ -573,7 +573,7 @@ def main():
     ap.add_argument("--no-hbm", dest="hbm", action="store_false", help="kernel mode: skip the LN / RoPE timings")
     ap.add_argument("--no-configs", dest="configs", action="store_false",
                     help="kernel mode: skip the cfg3 / cfg5 legs (one GPU only)")
-    ap.add_argument("--cfg-steps", type=int, default=4, help="timed steps of each cfg3 / cfg5 leg")
+    ap.add_argument("--cfg-steps", type=int, default=6, help="timed steps of each cfg3 / cfg5 leg")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--traffic", type=float, default=None,
                     help="HBM bytes per dominant-kernel launch from rocprofv3 PMC (profiles/)")

@@ -31,6 +31,17 @@ def _randomise_lambdas(m, seed=3):
                 p.copy_(torch.randn(p.shape, generator=g) * 0.1)
 
 
+def _log(name, rows):
+    import json
+    import os
+    d = os.environ.get("DTA_TEST_LOG_DIR")
+    if d:
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, name + ".json"), "w") as f:
+            for r in rows:
+                f.write(json.dumps(r) + "\n")
+
+
 def _oracle_diff_transformer(sd, idx, tgt, n_head, n_layer, block):
     """DiffTransformer.forward (diff_transformer.py:154-175) with Block.forward (:123-126)
     and SwiGLU (:95-105), on the oracle's MultiHeadDiffAttention restatement."""
@@ -98,9 +109,24 @@ def test_default_config_diff_transformer_bf16_autocast():
     loss.backward()
     torch.cuda.synchronize()
     assert rel_err(logits.float().cpu(), ref_logits.detach()) < 2e-2
+    # Through two blocks of bf16 GEMMs and LayerNorms a weight gradient carries more than one
+    # bf16 rounding: the bar is 2e-2 or, where larger, 2x the error of the reference
+    # algorithm itself run under the same bf16 autocast (the oracle model on the GPU), as in
+    # test_gpu_modules.test_module_bf16_autocast; every error and bar is logged.
+    sd32 = {k: v.detach().float().to(DEV).requires_grad_(True) for k, v in sd.items()}
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        _, l32 = _oracle_diff_transformer(sd32, idx.to(DEV), tgt.to(DEV), 4, 2, 512)
+    l32.backward()
+    log = []
     for n, p in m.named_parameters():
-        if ".diff_attn." in n and "lambda_" not in n:        # lambda bars: test_gpu_modules BF16_LOOSE
-            assert rel_err(p.grad.double().cpu(), sd[n].grad) < 2e-2, (n, rel_err(p.grad.double().cpu(), sd[n].grad))
+        if ".diff_attn." not in n:
+            continue
+        err = rel_err(p.grad.double().cpu(), sd[n].grad)
+        ref_err = rel_err(sd32[n].grad.double().cpu(), sd[n].grad)
+        bar = max(2e-2, 2.0 * ref_err)
+        log.append({"param": n, "err": err, "ref_alg_bf16_err": ref_err, "bar": bar})
+        assert err < bar, (n, err, ref_err)
+    _log("bf16_grad_errors_default_config_model", log)
 
 
 @pytest.mark.parametrize("n_terms", [2, 3, 4])
