@@ -558,9 +558,8 @@ void attn_fwd_kernel(FwdParams p) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int tid = threadIdx.x, lane = tid & 63;
   int hf = lane >> 5, c32 = lane & 31;
-  const int nblk = gridDim.x * gridDim.y * gridDim.z;
-  const int lin = xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z), nblk);
-  const int bx = lin % gridDim.x, by = (lin / gridDim.x) % gridDim.y, bz = lin / (gridDim.x * gridDim.y);
+  int bx, by, bz, lin;
+  lpt_order(bx, by, bz, lin);                          // bx: work rank
   const int nch = p.DV / DVC;
   const int qt = gridDim.x - 1 - bx;                   // longest causal rows first
   const int hh = by / nch, dc0 = (by % nch) * DVC;
@@ -926,10 +925,9 @@ void attn_dq_kernel(BwdParams p) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int tid = threadIdx.x, lane = tid & 63;
   int hf = lane >> 5, c32 = lane & 31;
-  const int nblk = gridDim.x * gridDim.y * gridDim.z;
-  const int lin = xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z), nblk);
-  const int bx = lin % gridDim.x, by = (lin / gridDim.x) % gridDim.y, bz = lin / (gridDim.x * gridDim.y);
-  const int qt = gridDim.x - 1 - bx;
+  int bx, by, bz, lin;
+  lpt_order(bx, by, bz, lin);                          // bx: work rank
+  const int qt = gridDim.x - 1 - bx;                   // longest causal rows first
   const int hh = by, b = bz;
   const int T = p.T;
   const int q0 = qt * BM, qw0 = q0 + wave * 32;
@@ -1388,10 +1386,9 @@ void attn_dkdv_kernel(BwdParams p) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int tid = threadIdx.x, lane = tid & 63;
   int hf = lane >> 5, c32 = lane & 31;
-  const int nblk = gridDim.x * gridDim.y * gridDim.z;
-  const int lin = xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z), nblk);
-  const int bx = lin % gridDim.x, by = (lin / gridDim.x) % gridDim.y, bz = lin / (gridDim.x * gridDim.y);
-  const int kblk = bx;                    // block 0 has the most query tiles: dispatched first
+  int bx, by, bz, lin;
+  lpt_order(bx, by, bz, lin);
+  const int kblk = bx;                    // key block 0 has the most query tiles: rank 0
   const int hh = by, b = bz;
   const int T = p.T;
   const int kb0 = kblk * BK, kw0 = kb0 + wave * 32;

@@ -52,6 +52,33 @@ __device__ __forceinline__ int xcd_remap(int id, int n) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + id / 8;
 }
 
+// Dispatch order of the attention grids (grid x = work rank, y / z = head, chunk, batch):
+// the work rank r (0 = the workgroups with the most causal tiles) varies slowest and the
+// (y, z) index fastest.  Blocks are dealt round-robin over the 8 XCDs, so every XCD starts
+// on its longest workgroups and ends on its shortest (longest-processing-time first: no
+// long workgroup is left running alone at the end of the grid), and, when gridDim.y *
+// gridDim.z is a multiple of 8, all workgroups of one (y, z) land on one XCD (its L2).
+// Speed only -- never correctness.
+#ifndef DTA_LPT
+#define DTA_LPT 1
+#endif
+__device__ __forceinline__ void lpt_order(int& r, int& y, int& z, int& id) {
+  id = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  if (DTA_LPT) {
+    const int nyz = gridDim.y * gridDim.z;
+    r = id / nyz;
+    const int rest = id - r * nyz;
+    y = rest % gridDim.y;
+    z = rest / gridDim.y;
+  } else {
+    const int lin = xcd_remap(id, gridDim.x * gridDim.y * gridDim.z);
+    r = lin % gridDim.x;
+    y = (lin / gridDim.x) % gridDim.y;
+    z = lin / (gridDim.x * gridDim.y);
+    id = lin;
+  }
+}
+
 template <class E> struct Ops;
 
 // ----------------------------------------------------------- 16-bit types ---
