@@ -32,6 +32,7 @@
 #include "dta_common.h"
 #include "dta_internal.h"
 
+#include <type_traits>
 #include <utility>
 
 #ifndef DTA_STAMPS
@@ -231,6 +232,21 @@ __device__ __forceinline__ void lgkm_pin(lds64 (&r)[M][4]) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(r[m][j]));
 }
+// Software-pipelined operand reads: ds_read_b128 by inline asm (invisible to the
+// compiler's waitcnt pass) and counted waits.  lgkmcnt(N) with N = the number of OUR reads
+// issued after the one being consumed is exact whatever else the compiler interleaves:
+// LDS returns in order, so any other LDS / SMEM op only makes the wait longer.
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+template <int OFF>
+__device__ __forceinline__ void ds128(i32x4& r, unsigned a) {
+  static_assert(OFF >= 0 && OFF < 65536, "DS immediate offset");
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(a), "i"(OFF));
+}
+template <int N>
+__device__ __forceinline__ void lgkm_wait() {
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(N) : "memory");
+}
+
 template <class E>
 __device__ __forceinline__ typename Ops<E>::frag tr_frag(const lds64 (&r)[4], int s) {
   typedef short v4s __attribute__((ext_vector_type(4)));
@@ -459,6 +475,29 @@ inline bool kv_layout_ok(const P& p, int es) {
   if (ks <= 0 || vs <= 0 || p.k.si < 0) return false;
   if ((int64_t)(p.N - 1) * p.k.si + p.HS > ks || p.DV > vs) return false;
   return (int64_t)p.T * ks * es < (1ll << 31) && (int64_t)p.T * vs * es < (1ll << 31);
+}
+
+// Row constants as an extra MFMA k-step (bf16, no dropout): each query row's constants
+// ride in the score and dP chains instead of one VALU op per element.  A = a "ones"
+// fragment (k = 0, 1 set), B = the row's constant split into two bf16 halves (hi, lo:
+// 16 significant bits), so every accumulator starts at that constant:
+//   S'_i = (sl2 Q_i) K_i^T - LSE_i      (Q_i pre-scaled by sl2 once per workgroup)
+//   dP'  = dO V^T - delta_0
+// P_i = exp2(S'_i) with no fma; dS_0 / c_0 = P_0 dP', dS_i / c_i = P_i (dP' + delta_0 -
+// delta_i); c_i and the softmax scale are applied once in the dQ epilogue.
+#ifndef DTA_DQ_SEED
+#define DTA_DQ_SEED 1
+#endif
+#ifndef DTA_DQ_PIPE
+#define DTA_DQ_PIPE 3
+#endif
+template <class E>
+__device__ __forceinline__ typename Ops<E>::frag seed_frag(float v, int hf) {
+  typename Ops<E>::frag f = Ops<E>::zero();
+  const E hi = (E)v;
+  const E lo = (E)(v - (float)hi);
+  if (hf == 0) { f[0] = hi; f[1] = lo; }
+  return f;
 }
 
 // ---------------------------------------------------------------- forward ---
@@ -961,6 +1000,8 @@ void attn_dq_kernel(BwdParams p) {
     }
   };
 
+  // (head size 128 at N >= 3 spills further with the seed fragments: it keeps the fmas)
+  constexpr bool SEED = DTA_DQ_SEED && std::is_same<E, __bf16>::value && !DROP && SRD && !(HS >= 128 && N >= 3);
   // ---- per-row operands in registers: Q_i and dO rows (B operands), LSE, delta
   frag qf[NQR > 0 ? NQR : 1][NQR > 0 ? NSQ : 1], df[NSV];
   float coef[N], lse[N], del[N];
@@ -977,6 +1018,12 @@ void attn_dq_kernel(BwdParams p) {
       for (int s = 0; s < NSQ; ++s)
         qf[i < NQR ? i : 0][s] = rowok ? O::load_global(gq + (int64_t)qrow * p.q.st + i * p.q.si + s * KS + hf * O::KH)
                                        : O::zero();
+      if constexpr (SEED) {
+#pragma unroll
+        for (int s = 0; s < NSQ; ++s)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) qf[i < NQR ? i : 0][s][j] = (E)((float)qf[i < NQR ? i : 0][s][j] * p.sl2);
+      }
     }
     lse[i] = rowok ? p.lse[rs + i * bstride] : 0.f;
     // delta_i = <dO, O_i> over this row (flash-backward preprocess), both lane halves
@@ -1022,6 +1069,22 @@ void attn_dq_kernel(BwdParams p) {
     if (j < ntiles) stage_kv(j, j);
   wait_vm(tile_pieces * max(0, min(NS - 1, ntiles) - 1));
   lds_barrier();
+  // SEED: the LDS-resident Q_i rows pre-scaled by sl2 once; the seed fragments
+  frag f_one = O::zero(), f_lse[SEED ? N : 1], f_dp = O::zero();
+  float ddel[N];
+  if constexpr (SEED) {
+    if constexpr (!QREG && N > NQR) {
+      scale_lds<E, NTHR>(Qs, CF::nQ, p.sl2, tid);
+      lds_barrier();
+    }
+    if (hf == 0) { f_one[0] = (E)1.f; f_one[1] = (E)1.f; }
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      f_lse[i] = seed_frag<E>(lse[i], hf);
+      ddel[i] = del[0] - del[i];
+    }
+    f_dp = seed_frag<E>(-del[0], hf);
+  }
 
   f32x16 dq[N][NHB];
 #pragma unroll
@@ -1074,7 +1137,24 @@ void attn_dq_kernel(BwdParams p) {
           const int Lv = LrV;
           const char* vbase = reinterpret_cast<const char*>(Vc);
 #pragma unroll
-          for (int kb = 0; kb < NKB; ++kb) dp[kb] = f32x16{};
+          for (int kb = 0; kb < NKB; ++kb) dp[kb] = SEED ? O::mma(f_one, f_dp, f32x16{}) : f32x16{};
+          if constexpr (XA && DTA_DQ_PIPE > 0) {
+            // V fragments read DTA_DQ_PIPE MFMAs ahead (k-step major, key block minor)
+            constexpr int NIT = NSV * NKB, D = DTA_DQ_PIPE;
+            i32x4 vb[D + 1];
+            auto issue = [&](auto J) {
+              constexpr int j = decltype(J)::value;
+              ds128<(j % NKB) * 32 * VI::ROWB>(vb[j % (D + 1)], bV ^ (32 * (j / NKB)));
+            };
+            sfor<(D < NIT ? D : NIT)>([&](auto J) { issue(J); });
+            sfor<NIT>([&](auto J) {
+              constexpr int j = decltype(J)::value;
+              if constexpr (j + D < NIT) issue(std::integral_constant<int, j + D>{});
+              lgkm_wait<(j + D < NIT ? D : NIT - 1 - j)>();
+              asm volatile("" : "+v"(vb[j % (D + 1)]));
+              dp[j % NKB] = O::mma(__builtin_bit_cast(frag, vb[j % (D + 1)]), df[j / NKB], dp[j % NKB]);
+            });
+          } else
 #pragma unroll
           for (int s = 0; s < NSV; ++s) {
             const int o = Lv ^ (32 * s);
@@ -1084,6 +1164,7 @@ void attn_dq_kernel(BwdParams p) {
               else dp[kb] = O::mma(*reinterpret_cast<const frag*>(vbase + kb * 32 * VI::ROWB + o), df[s], dp[kb]);
             }
           }
+
         } else {
 #pragma unroll
           for (int kb = 0; kb < NKB; ++kb) {
@@ -1092,18 +1173,54 @@ void attn_dq_kernel(BwdParams p) {
             for (int s = 0; s < NSV; ++s) dp[kb] = O::mma(VI::row(Vc, kb * 32 + c32, s, hf), df[s], dp[kb]);
           }
         }
-#pragma unroll
-        for (int i = 0; i < N; ++i) {
+        sfor<N>([&](auto I_) {
+          constexpr int i = decltype(I_)::value;
           const E* Ki = Kc + i * BN * HSP;
           f32x16 sa[NKB];
-          if constexpr (sizeof(E) == 2) {
+          if constexpr (XA && DTA_DQ_PIPE > 0) {
+            // S'_i chain with its operand reads DTA_DQ_PIPE reads ahead of the MFMAs: per
+            // k-step s the Q_i fragment (LDS-resident branches) then the NKB K_i fragments
+            constexpr int QL = i >= NQR ? 1 : 0, PER = NKB + QL, NR = NSQ * PER, D = DTA_DQ_PIPE;
+            constexpr int KOFF = i * BN * HSP * (int)sizeof(E), QOFF = (i >= NQR ? i - NQR : 0) * BM * QP * (int)sizeof(E);
+            i32x4 kr[D + 1], qv[QL ? NSQ : 1];
+            const unsigned bQ = lds_addr(Qs) + wave * 32 * QI::ROWB + LrQ;
+            auto issue = [&](auto J) {
+              constexpr int j = decltype(J)::value, st = j / PER, w = j % PER;
+              if constexpr (QL && w == 0) ds128<QOFF>(qv[QL ? st : 0], bQ ^ (32 * st));
+              else ds128<KOFF + (w - QL) * 32 * KI::ROWB>(kr[(st * NKB + w - QL) % (D + 1)], bK ^ (32 * st));
+            };
+#pragma unroll
+            for (int kb = 0; kb < NKB; ++kb) sa[kb] = SEED ? O::mma(f_one, f_lse[SEED ? i : 0], f32x16{}) : f32x16{};
+            sfor<(D < NR ? D : NR)>([&](auto J) { issue(J); });
+            sfor<NSQ * NKB>([&](auto C) {
+              constexpr int c = decltype(C)::value, st = c / NKB, kb = c % NKB;
+              constexpr int j = st * PER + QL + kb;                  // read index of this K fragment
+              // keep D reads in flight past the one consumed
+              sfor<NR>([&](auto J2) {
+                constexpr int j2 = decltype(J2)::value;
+                if constexpr (j2 >= D && j2 <= j + D - (c == 0 ? 0 : 0) && j2 > (c == 0 ? D - 1 : (((c - 1) / NKB) * PER + QL + (c - 1) % NKB) + D))
+                  issue(std::integral_constant<int, j2>{});
+              });
+              constexpr int issued = (j + D + 1 < NR ? j + D + 1 : NR);
+              lgkm_wait<issued - 1 - j>();
+              asm volatile("" : "+v"(kr[c % (D + 1)]));
+              frag qb;
+              if constexpr (QL) {
+                asm volatile("" : "+v"(qv[QL ? st : 0]));
+                qb = __builtin_bit_cast(frag, qv[QL ? st : 0]);
+              } else {
+                qb = qf[i < NQR ? i : 0][st];
+              }
+              sa[kb] = O::mma(__builtin_bit_cast(frag, kr[c % (D + 1)]), qb, sa[kb]);
+            });
+          } else if constexpr (sizeof(E) == 2) {
             const int Lr = LrK;
             const char* kbase = reinterpret_cast<const char*>(Ki);
             const char* qbase = reinterpret_cast<const char*>(Qs + (i >= NQR ? i - NQR : 0) * BM * QP) +
                                 wave * 32 * QI::ROWB;
             const int Lq = LrQ;
 #pragma unroll
-            for (int kb = 0; kb < NKB; ++kb) sa[kb] = f32x16{};
+            for (int kb = 0; kb < NKB; ++kb) sa[kb] = SEED ? O::mma(f_one, f_lse[SEED ? i : 0], f32x16{}) : f32x16{};
 #pragma unroll
             for (int s = 0; s < NSQ; ++s) {
               frag qb;
@@ -1134,6 +1251,19 @@ void attn_dq_kernel(BwdParams p) {
           // dS^T = c_i P^T (dP^T - delta_i) = P^T * (c_i dP^T - c_i delta_i)
           const float li = lse[i], ci = coef[i], cdi = coef[i] * del[i];
           const int lim = min(qrow, T - 1) - k0 - 4 * hf;
+          if constexpr (SEED) {
+            // sa = S'_i (seeded with -LSE_i), dp = dP - delta_0: dS_i / c_i
+            const float dd = ddel[i];
+#pragma unroll
+            for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+              for (int r = 0; r < 16; ++r) {
+                float arg = sa[kb][r];
+                if constexpr (MASK) arg = (kb * 32 + (r & 3) + 8 * (r >> 2) > lim) ? -INFINITY : arg;
+                const float pr = exp2_fast(arg);
+                sa[kb][r] = i == 0 ? pr * dp[kb][r] : pr * (dp[kb][r] + dd);
+              }
+          } else {
           uint32_t dkey = 0;
           if constexpr (DROP) dkey = drop_key(p.drop_seed_lo, p.drop_seed_hi, b, hh, i, p.H, N);
 #pragma unroll
@@ -1148,6 +1278,7 @@ void attn_dq_kernel(BwdParams p) {
                 cm *= drop_mul(dkey, qrow, k0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hf, p.drop_thr, p.drop_scale);
               sa[kb][r] = exp2_fast(arg) * fmaf(cm, dp[kb][r], -cdi);
             }
+          }
           // dQ_i^T += K_i^T dS_i^T
           if constexpr (sizeof(E) == 2) {
             const unsigned kbse = lds_addr(Ki);
@@ -1175,7 +1306,7 @@ void attn_dq_kernel(BwdParams p) {
                 for (int s = 0; s < SPB; ++s)
                   dq[i][d] = O::mma(KI::tr_perm(Ki, kb * 32, s, hf, d * 32, lane), sa[kb][s], dq[i][d]);
           }
-        }
+        });
       }
     }
     wait_vm(tile_pieces * max(0, min(NS - 2, ntiles - 2 - kt)));
@@ -1194,8 +1325,9 @@ void attn_dq_kernel(BwdParams p) {
       for (int g = 0; g < 4; ++g) {
         const int e = d * 32 + 8 * g + 4 * hf;
         if (e >= HS) continue;
-        float a0 = dq[i][d][4 * g] * p.scale, a1 = dq[i][d][4 * g + 1] * p.scale;
-        float a2 = dq[i][d][4 * g + 2] * p.scale, a3 = dq[i][d][4 * g + 3] * p.scale;
+        const float sc = SEED ? p.scale * coef[i] : p.scale;
+        float a0 = dq[i][d][4 * g] * sc, a1 = dq[i][d][4 * g + 1] * sc;
+        float a2 = dq[i][d][4 * g + 2] * sc, a3 = dq[i][d][4 * g + 3] * sc;
         if (p.rope) rope_inv4(p.rope, qrow, HS, e, a0, a1, a2, a3);
         if constexpr (OUTF32) {
           store4<float>(p.dq32 + ((((int64_t)b * T + qrow) * p.H + hh) * N + i) * HS + e, a0, a1, a2, a3);
