@@ -247,6 +247,60 @@ __device__ __forceinline__ void lgkm_wait() {
   asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(N) : "memory");
 }
 
+// One score chain S[kb] += K[kb] Q^T over NSQ k-steps (32-row key blocks kb < NKB, K rows as
+// the A operand) with every operand read D reads ahead of its MFMA.  Per k-step s: the Q
+// fragment (QL: from LDS at bQ ^ 32 s + QOFF, else qreg[s]) then the NKB K fragments
+// (bK ^ 32 s + KOFF + kb * 32 * KROWB).  bK / bQ: lane bases whose bits 5..6 are the lane's
+// own (the XOR applies to them; the region offsets ride in DS immediates).
+template <class E, int NSQ, int NKB, int QL, int D, int KOFF, int QOFF, int KROWB>
+__device__ __forceinline__ void s_chain_pipe(f32x16 (&sa)[NKB], unsigned bK, unsigned bQ,
+                                             const typename Ops<E>::frag* qreg) {
+  using frag = typename Ops<E>::frag;
+  constexpr int PER = NKB + QL, NR = NSQ * PER;
+  // region offsets past the 16-bit DS immediate go into the base (they are multiples of a
+  // tile, so the k-step XOR still applies after the add)
+  constexpr bool KBIG = KOFF + NKB * 32 * KROWB >= 65536, QBIG = QOFF + 1024 >= 65536;
+  bK += KBIG ? KOFF : 0;
+  bQ += QBIG ? QOFF : 0;
+  i32x4 kr[D + 1], qv[QL ? NSQ : 1];
+  auto issue = [&](auto J) {
+    constexpr int j = decltype(J)::value, st = j / PER, w = j % PER;
+    if constexpr (QL && w == 0) ds128<(QBIG ? 0 : QOFF)>(qv[QL ? st : 0], bQ ^ (32 * st));
+    else ds128<(KBIG ? 0 : KOFF) + (w - QL) * 32 * KROWB>(kr[(st * NKB + w - QL) % (D + 1)], bK ^ (32 * st));
+  };
+  sfor<(D < NR ? D : NR)>([&](auto J) { issue(J); });
+  sfor<NSQ * NKB>([&](auto C) {
+    constexpr int c = decltype(C)::value, st = c / NKB, kb = c % NKB;
+    constexpr int j = st * PER + QL + kb;                                   // this K fragment's read
+    constexpr int from = c == 0 ? D : ((c - 1) / NKB) * PER + QL + (c - 1) % NKB + D + 1;
+    sfor<NR>([&](auto J2) {                                                   // reads (from, j + D]
+      constexpr int j2 = decltype(J2)::value;
+      if constexpr (j2 >= from && j2 <= j + D) issue(std::integral_constant<int, j2>{});
+    });
+    constexpr int issued = (j + D + 1 < NR ? j + D + 1 : NR);
+    lgkm_wait<issued - 1 - j>();
+    asm volatile("" : "+v"(kr[c % (D + 1)]));
+    frag qb;
+    if constexpr (QL) {
+      asm volatile("" : "+v"(qv[QL ? st : 0]));
+      qb = __builtin_bit_cast(frag, qv[QL ? st : 0]);
+    } else {
+      qb = qreg[st];
+    }
+    sa[kb] = Ops<E>::mma(__builtin_bit_cast(frag, kr[c % (D + 1)]), qb, sa[kb]);
+  });
+}
+
+// lgkm_pin with CNT younger reads left in flight
+template <int CNT, int M>
+__device__ __forceinline__ void lgkm_pin_n(lds64 (&r)[M][4]) {
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(CNT) : "memory");
+#pragma unroll
+  for (int m = 0; m < M; ++m)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(r[m][j]));
+}
+
 template <class E>
 __device__ __forceinline__ typename Ops<E>::frag tr_frag(const lds64 (&r)[4], int s) {
   typedef short v4s __attribute__((ext_vector_type(4)));
@@ -490,6 +544,12 @@ inline bool kv_layout_ok(const P& p, int es) {
 #endif
 #ifndef DTA_DQ_PIPE
 #define DTA_DQ_PIPE 3
+#endif
+#ifndef DTA_FWD_PIPE
+#define DTA_FWD_PIPE 3
+#endif
+#ifndef DTA_DKDV_FUSE1
+#define DTA_DKDV_FUSE1 1
 #endif
 template <class E>
 __device__ __forceinline__ typename Ops<E>::frag seed_frag(float v, int hf) {
@@ -773,6 +833,17 @@ void attn_fwd_kernel(FwdParams p) {
           if (i < NQR) __builtin_amdgcn_sched_group_barrier(0x100, NSQ * NKB, 0);
           else __builtin_amdgcn_sched_group_barrier(0x100, NSQ * (NKB + 1), 0);
           __builtin_amdgcn_sched_group_barrier(0x008, NSQ * NKB, 0);
+        } else if constexpr (DTA_FWD_PIPE > 0 && QI::ROWB == KI::ROWB && NKB == 1) {
+          // operand reads DTA_FWD_PIPE reads ahead of the MFMAs (see s_chain_pipe); 32-key
+          // tiles only: with 64-key tiles (cfg2) the paired plan sits at 252 VGPRs and the
+          // pipelined chain measured slower (fwd 0.954 -> 1.008 ms), cfg5 0.97x
+          sfor<N>([&](auto I_) {
+            constexpr int ic = decltype(I_)::value;
+            if (ic == i)
+              s_chain_pipe<E, NSQ, NKB, (ic >= NQR ? 1 : 0), DTA_FWD_PIPE, ic * BN * HSP * (int)sizeof(E),
+                           (ic >= NQR ? ic - NQR : 0) * BM * HSP * (int)sizeof(E), KI::ROWB>(
+                  sa[ic], lds_addr(Kc) + Lr, lds_addr(Qs) + wave * 32 * QI::ROWB + Lr, qf[ic < NQR ? ic : 0]);
+          });
         } else {
 #pragma unroll
           for (int s = 0; s < NSQ; ++s) {
@@ -804,7 +875,32 @@ void attn_fwd_kernel(FwdParams p) {
   // O_i^T += V^T P_i^T, one V fragment feeds every branch
   auto phase_b = [&](int kt, const frag (&pf)[N][NKB * SPB]) {
     const E* Vc = Vb + (kt % NS) * CF::nV;
-    if constexpr (sizeof(E) == 2) {
+    if constexpr (sizeof(E) == 2 && DTA_FWD_PIPE > 0 && NKB == 1 && NDB > 1) {
+      // the next d-block's V^T fragments read while this one's MFMAs run (32-key tiles:
+      // 8 more VGPRs)
+      const unsigned vb = lds_addr(Vc);
+      const int Lv = LtV;
+      lds64 r[2][NKB][4];
+      auto issue = [&](auto D) {
+        constexpr int d = decltype(D)::value;
+        const unsigned a0 = vb + (Lv ^ (64 * d)), a1 = vb + (Lv ^ (64 * d + 32));
+        sfor<NKB>([&](auto KB) { tr_issue<VI::ROWB, 32 * decltype(KB)::value>(r[d & 1][decltype(KB)::value], a0, a1); });
+      };
+      issue(std::integral_constant<int, 0>{});
+      sfor<NDB>([&](auto D) {
+        constexpr int d = decltype(D)::value;
+        if constexpr (d + 1 < NDB) issue(std::integral_constant<int, d + 1>{});
+        lgkm_pin_n<(d + 1 < NDB ? 4 * NKB : 0), NKB>(r[d & 1]);
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            const frag va = tr_frag<E>(r[d & 1][kb], s);
+#pragma unroll
+            for (int i = 0; i < N; ++i) acc[i][d] = O::mma(va, pf[i][kb * 2 + s], acc[i][d]);
+          }
+      });
+    } else if constexpr (sizeof(E) == 2) {
       const unsigned vb = lds_addr(Vc);
       const int Lv = LtV;
       sfor<NDB>([&](auto D) {
@@ -1178,41 +1274,13 @@ void attn_dq_kernel(BwdParams p) {
           const E* Ki = Kc + i * BN * HSP;
           f32x16 sa[NKB];
           if constexpr (XA && DTA_DQ_PIPE > 0) {
-            // S'_i chain with its operand reads DTA_DQ_PIPE reads ahead of the MFMAs: per
-            // k-step s the Q_i fragment (LDS-resident branches) then the NKB K_i fragments
-            constexpr int QL = i >= NQR ? 1 : 0, PER = NKB + QL, NR = NSQ * PER, D = DTA_DQ_PIPE;
+            // S'_i chain with its operand reads DTA_DQ_PIPE reads ahead of the MFMAs
+            constexpr int QL = i >= NQR ? 1 : 0;
             constexpr int KOFF = i * BN * HSP * (int)sizeof(E), QOFF = (i >= NQR ? i - NQR : 0) * BM * QP * (int)sizeof(E);
-            i32x4 kr[D + 1], qv[QL ? NSQ : 1];
-            const unsigned bQ = lds_addr(Qs) + wave * 32 * QI::ROWB + LrQ;
-            auto issue = [&](auto J) {
-              constexpr int j = decltype(J)::value, st = j / PER, w = j % PER;
-              if constexpr (QL && w == 0) ds128<QOFF>(qv[QL ? st : 0], bQ ^ (32 * st));
-              else ds128<KOFF + (w - QL) * 32 * KI::ROWB>(kr[(st * NKB + w - QL) % (D + 1)], bK ^ (32 * st));
-            };
 #pragma unroll
             for (int kb = 0; kb < NKB; ++kb) sa[kb] = SEED ? O::mma(f_one, f_lse[SEED ? i : 0], f32x16{}) : f32x16{};
-            sfor<(D < NR ? D : NR)>([&](auto J) { issue(J); });
-            sfor<NSQ * NKB>([&](auto C) {
-              constexpr int c = decltype(C)::value, st = c / NKB, kb = c % NKB;
-              constexpr int j = st * PER + QL + kb;                  // read index of this K fragment
-              // keep D reads in flight past the one consumed
-              sfor<NR>([&](auto J2) {
-                constexpr int j2 = decltype(J2)::value;
-                if constexpr (j2 >= D && j2 <= j + D - (c == 0 ? 0 : 0) && j2 > (c == 0 ? D - 1 : (((c - 1) / NKB) * PER + QL + (c - 1) % NKB) + D))
-                  issue(std::integral_constant<int, j2>{});
-              });
-              constexpr int issued = (j + D + 1 < NR ? j + D + 1 : NR);
-              lgkm_wait<issued - 1 - j>();
-              asm volatile("" : "+v"(kr[c % (D + 1)]));
-              frag qb;
-              if constexpr (QL) {
-                asm volatile("" : "+v"(qv[QL ? st : 0]));
-                qb = __builtin_bit_cast(frag, qv[QL ? st : 0]);
-              } else {
-                qb = qf[i < NQR ? i : 0][st];
-              }
-              sa[kb] = O::mma(__builtin_bit_cast(frag, kr[c % (D + 1)]), qb, sa[kb]);
-            });
+            s_chain_pipe<E, NSQ, NKB, QL, DTA_DQ_PIPE, KOFF, QOFF, KI::ROWB>(
+                sa, bK, lds_addr(Qs) + wave * 32 * QI::ROWB + LrQ, qf[i < NQR ? i : 0]);
           } else if constexpr (sizeof(E) == 2) {
             const int Lr = LrK;
             const char* kbase = reinterpret_cast<const char*>(Ki);
@@ -1413,8 +1481,10 @@ struct TileRing {
       } else {
         if (j < PQ) buf_lds16(bq, nq, st0 + j * 1024, off[u]);
         else if (j < PQ + PD) buf_lds16(bd, nd, st0 + OFF_D + (j - PQ) * 1024, off[u]);
+#ifndef DTA_DKDV_NOROWS_PROBE
         else if (j < PQ + PD + PL) buf_lds4(lse + q0, nl, st0 + OFF_L + (j - PQ - PD) * 256, off[u]);
         else if (j < NPC) buf_lds4(delta + q0, nl, st0 + OFF_G + (j - PQ - PD - PL) * 256, off[u]);
+#endif
       }
     });
   }
@@ -1920,7 +1990,11 @@ int launch_dkdv_t(const BwdParams& p, hipStream_t st) {
   constexpr int bytes = CF::bytes;
   dim3 grid((p.T + NW * 32 - 1) / (NW * 32), p.H, p.B);
   dim3 block(NW * 64);
-  constexpr bool FUSED = DkdvSplit<HS, N, DV>::fused;
+  // one-wave-per-SIMD 16-bit plans (4 waves, not paired) have 512 registers: dK and dV
+  // accumulators up to 288 of them share one launch (head size 128 at N = 2, cfg5)
+  constexpr int HSB = DkdvSplit<HS, N, DV>::HSB;
+  constexpr bool FUSED = DkdvSplit<HS, N, DV>::fused ||
+                         (DTA_DKDV_FUSE1 && sizeof(E) == 2 && NW == 4 && !PR && N * HSB / 2 + DV / 2 <= 288);
   auto run = [&](auto DKV, auto DVVV, auto SRDV) -> int {
     auto kern = attn_dkdv_kernel<E, HS, N, DV, NW, decltype(DKV)::value, decltype(DVVV)::value, decltype(SRDV)::value,
                                  DROP, PR, GR>;

@@ -46,10 +46,25 @@ __device__ __forceinline__ void st8(E* p, const float* f) {
   }
 }
 
+// Sum over the 64 lanes, every lane gets the total: four DPP steps inside each 16-lane
+// row (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror), then
+// v_permlane16_swap and v_permlane32_swap across rows -- all VALU, where __shfl_xor took
+// six ds_bpermute round trips through the LDS, each behind an lgkmcnt(0) wait.
+template <int CTRL>
+__device__ __forceinline__ float dpp_add(float v) {
+  return v + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
+}
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v = dpp_add<0xB1>(v);      // quad_perm [1,0,3,2]
+  v = dpp_add<0x4E>(v);      // quad_perm [2,3,0,1]
+  v = dpp_add<0x141>(v);     // row_half_mirror
+  v = dpp_add<0x140>(v);     // row_mirror
+  const unsigned u = __float_as_uint(v);
+  auto r16 = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+  v = __uint_as_float(r16[0]) + __uint_as_float(r16[1]);
+  const unsigned w = __float_as_uint(v);
+  auto r32 = __builtin_amdgcn_permlane32_swap(w, w, false, false);
+  return __uint_as_float(r32[0]) + __uint_as_float(r32[1]);
 }
 
 
@@ -256,19 +271,26 @@ __global__ __launch_bounds__(256) void ln_bwd_rb_kernel(LnParams p) {
   constexpr int NR = P16 ? 1 : 2, NY = Y16 ? 1 : 2;
   RT xr[2][CHB][NR];
   RY dr[2][CHB][NY];
+  float mr[2], rr[2];
   auto load = [&](auto S, int64_t r) {
     constexpr int s = decltype(S)::value;
+    // the row statistics first: a load issued after the next row's prefetch would make
+    // its wait (vmcnt counts in order) drain that prefetch too
+    mr[s] = p.mean[r];
+    rr[s] = p.rstd[r];
     const E* x = reinterpret_cast<const E*>(p.x) + r * p.xs;
     const Y* dy = reinterpret_cast<const Y*>(p.dy) + r * p.dys;
+    // unconditional loads (lanes past C read column 0, masked in the math): a load behind a
+    // divergent branch leaves the wait counters unknown at the join, and the compiler
+    // then waits for every load in flight -- the next row's prefetch included
 #pragma unroll
     for (int c = 0; c < CHB; ++c) {
-      const int col = (c * 256 + t) * 8;
-      if (col < p.C) {
+      const int col0 = (c * 256 + t) * 8;
+      const int col = col0 < p.C ? col0 : 0;
 #pragma unroll
-        for (int k = 0; k < NR; ++k) xr[s][c][k] = *reinterpret_cast<const RT*>(x + col + k * 4);
+      for (int k = 0; k < NR; ++k) xr[s][c][k] = *reinterpret_cast<const RT*>(x + col + k * 4);
 #pragma unroll
-        for (int k = 0; k < NY; ++k) dr[s][c][k] = *reinterpret_cast<const RY*>(dy + col + k * 4);
-      }
+      for (int k = 0; k < NY; ++k) dr[s][c][k] = *reinterpret_cast<const RY*>(dy + col + k * 4);
     }
   };
   auto cvt = [&](auto T16, const auto& v, float* f) {
@@ -282,38 +304,44 @@ __global__ __launch_bounds__(256) void ln_bwd_rb_kernel(LnParams p) {
   };
   const int64_t stride = gridDim.x;
   int par = 0;
+  // this thread's LN weights, the same for every row: loaded once (a per-row load issued
+  // behind the next row's prefetch would drain it at its wait)
+  float wv[CHB][8];
+#pragma unroll
+  for (int c = 0; c < CHB; ++c) {
+    const int col = (c * 256 + t) * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) wv[c][j] = col < p.C ? p.w[col + j] : 0.f;
+  }
   auto body = [&](auto S, int64_t r) {
     constexpr int s = decltype(S)::value;
+    const float mean = mr[s], rstd = rr[s];
     if (r + stride < p.rows) load(std::integral_constant<int, 1 - s>{}, r + stride);   // next row in flight
-    const float mean = p.mean[r], rstd = p.rstd[r];
     float xh[CHB][8], g[CHB][8];
     float sg = 0.f, sgx = 0.f;
 #pragma unroll
     for (int c = 0; c < CHB; ++c) {
-      const int col = (c * 256 + t) * 8;
-      if (col < p.C) {
-        float xv[8], dv[8];
-        cvt(E{}, xr[s][c], xv);
-        cvt(Y{}, dr[s][c], dv);
+      const bool ok = (c * 256 + t) * 8 < p.C;
+      float xv[8], dv[8];
+      cvt(E{}, xr[s][c], xv);
+      cvt(Y{}, dr[s][c], dv);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          xh[c][j] = (xv[j] - mean) * rstd;
-          const float dys = dv[j] * p.out_scale;
-          dwp[c][j] = fmaf(dys, xh[c][j], dwp[c][j]);
-          dbp[c][j] += dys;
-          g[c][j] = dys * p.w[col + j];
-          sg += g[c][j];
-          sgx = fmaf(g[c][j], xh[c][j], sgx);
-        }
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) { xh[c][j] = 0.f; g[c][j] = 0.f; }
+      for (int j = 0; j < 8; ++j) {
+        xh[c][j] = ok ? (xv[j] - mean) * rstd : 0.f;
+        const float dys = ok ? dv[j] * p.out_scale : 0.f;
+        dwp[c][j] = fmaf(dys, xh[c][j], dwp[c][j]);
+        dbp[c][j] += dys;
+        g[c][j] = dys * wv[c][j];
+        sg += g[c][j];
+        sgx = fmaf(g[c][j], xh[c][j], sgx);
       }
     }
     sg = wave_sum(sg);
     sgx = wave_sum(sgx);
     if (lane == 0) { red[par][wave][0] = sg; red[par][wave][1] = sgx; }
-    __syncthreads();
+    // LDS-only barrier: __syncthreads() would also wait for the next row's prefetch
+    __builtin_amdgcn_s_waitcnt(0xC07F);          // lgkmcnt(0)
+    __builtin_amdgcn_s_barrier();
     const float mg = (red[par][0][0] + red[par][1][0] + red[par][2][0] + red[par][3][0]) * inv_c;
     const float mgx = (red[par][0][1] + red[par][1][1] + red[par][2][1] + red[par][3][1]) * inv_c;
     par ^= 1;
