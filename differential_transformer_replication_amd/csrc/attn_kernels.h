@@ -661,19 +661,23 @@ void attn_fwd_kernel(FwdParams p) {
   lpt_order(bx, by, bz, lin);                          // bx: work rank
   const int nch = p.DV / DVC;
   const int qt = gridDim.x - 1 - bx;                   // longest causal rows first
-  const int hh = by / nch, dc0 = (by % nch) * DVC;
+  // branch-split launch (N == 1 instantiation, p.bsplit branches per head): workgroup
+  // (head, branch br) computes O_br and LSE_br only; a combine pass forms O
+  const int nsp = (N == 1 && p.bsplit > 1) ? p.bsplit : 1;
+  const int hv = by / nch, dc0 = (by % nch) * DVC;
+  const int hh = nsp > 1 ? hv / nsp : hv, br = hv - hh * nsp;
   const int b = bz;
   const int T = p.T;
   const int q0 = qt * BM, qw0 = q0 + wave * 32;
   int qrow = qw0 + c32;
 
-  const E* gq = reinterpret_cast<const E*>(p.q.p) + b * p.q.sb + hh * p.q.sh;
-  const E* gk = reinterpret_cast<const E*>(p.k.p) + b * p.k.sb + hh * p.k.sh;
+  const E* gq = reinterpret_cast<const E*>(p.q.p) + b * p.q.sb + hh * p.q.sh + br * p.q.si;
+  const E* gk = reinterpret_cast<const E*>(p.k.p) + b * p.k.sb + hh * p.k.sh + br * p.k.si;
   const E* gv = reinterpret_cast<const E*>(p.v.p) + b * p.v.sb + hh * p.v.sh + dc0;
 
   float coef[N];
 #pragma unroll
-  for (int i = 0; i < N; ++i) coef[i] = p.coef[hh * N + i];
+  for (int i = 0; i < N; ++i) coef[i] = nsp > 1 ? 1.f : p.coef[hh * N + i];
 
   frag qf[NQR > 0 ? NQR : 1][NQR > 0 ? NSQ : 1];
 #pragma unroll
@@ -764,7 +768,7 @@ void attn_fwd_kernel(FwdParams p) {
       }
     l[i] += ls0 + ls1;
     if constexpr (DROP) {
-      const uint32_t key = drop_key(p.drop_seed_lo, p.drop_seed_hi, b, hh, i, p.H, N);
+      const uint32_t key = drop_key(p.drop_seed_lo, p.drop_seed_hi, b, hh, br + i, p.H, nsp > 1 ? nsp : N);
 #pragma unroll
       for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
@@ -974,10 +978,10 @@ void attn_fwd_kernel(FwdParams p) {
     const float lt = wave_sum_halves(l[i]);
     inv[i] = 1.f / lt;
     if (dc0 == 0 && hf == 0)
-      p.lse[(((int64_t)i * p.B + b) * p.H + hh) * T + qrow] = -(m[i] + __builtin_log2f(lt));   // stored negated
+      p.lse[(((int64_t)(br + i) * p.B + b) * p.H + hh) * T + qrow] = -(m[i] + __builtin_log2f(lt));   // stored negated
   }
   E* go = reinterpret_cast<E*>(p.o.p) + b * p.o.sb + (int64_t)qrow * p.o.st + hh * p.o.sh + dc0;
-  E* gob = reinterpret_cast<E*>(p.obr.p) + b * p.obr.sb + (int64_t)qrow * p.obr.st + hh * p.obr.sh + dc0;
+  E* gob = reinterpret_cast<E*>(p.obr.p) + b * p.obr.sb + (int64_t)qrow * p.obr.st + hh * p.obr.sh + br * p.obr.si + dc0;
 #pragma unroll
   for (int d = 0; d < NDB; ++d)
 #pragma unroll
@@ -992,7 +996,7 @@ void attn_fwd_kernel(FwdParams p) {
         o0 = fmaf(coef[i], a0, o0); o1 = fmaf(coef[i], a1, o1);
         o2 = fmaf(coef[i], a2, o2); o3 = fmaf(coef[i], a3, o3);
       }
-      store4<E>(go + e, o0, o1, o2, o3);
+      if (nsp == 1) store4<E>(go + e, o0, o1, o2, o3);
     }
 }
 
@@ -1918,6 +1922,56 @@ static inline int set_smem(K kernel, int bytes) {
   return 0;
 }
 
+// O = sum_i c_i O_i after a branch-split forward (HBM-bound: N + 1 passes of
+// B*T*H*dv elements).  One thread per 16 bytes of an output row, fp32 sums.
+template <class E, int N>
+__global__ __launch_bounds__(256) void branch_combine_kernel(FwdParams p) {
+  constexpr int V = 16 / (int)sizeof(E);
+  typedef float f32xv __attribute__((ext_vector_type(V)));
+  typedef E ev __attribute__((ext_vector_type(V)));
+  const int vpr = p.DV / V;                                 // 16-byte vectors per (b, t, h) row
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t rows = (int64_t)p.B * p.T * p.H;
+  if (idx >= rows * vpr) return;
+  const int64_t row = idx / vpr;
+  const int e = (int)(idx - row * vpr) * V;
+  const int hh = (int)(row % p.H);
+  const int64_t bt = row / p.H;
+  const int t = (int)(bt % p.T), b = (int)(bt / p.T);
+  const E* src = reinterpret_cast<const E*>(p.obr.p) + b * p.obr.sb + (int64_t)t * p.obr.st + hh * p.obr.sh + e;
+  f32xv acc = f32xv{};
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const ev x = *reinterpret_cast<const ev*>(src + i * p.obr.si);
+    const float c = p.coef[hh * N + i];
+#pragma unroll
+    for (int j = 0; j < V; ++j) acc[j] = fmaf(c, (float)x[j], acc[j]);
+  }
+  ev y;
+#pragma unroll
+  for (int j = 0; j < V; ++j) y[j] = (E)acc[j];
+  *reinterpret_cast<ev*>(reinterpret_cast<E*>(p.o.p) + b * p.o.sb + (int64_t)t * p.o.st + hh * p.o.sh + e) = y;
+}
+
+// Branch-split forward policy: workgroups that hold ONE branch over the whole dv instead
+// of all N branches over a dv chunk.  Auto (DTA_FWD_BSPLIT unset / -1): wherever the
+// N-branch plan splits dv into chunks (each chunk redoes every branch's QK^T and
+// softmax: head size 128 at N = 2, cfg5; N = 4 at head size 64, cfg3) or runs one wave
+// per SIMD (N = 3 at head size 64, cfg3).  One-process A/B (profiles/r03_bsplit_ab.json):
+// cfg5 fwd 20.54 -> 12.66 ms, cfg3 N=4 0.744 -> 0.485, N=3 0.409 -> 0.361; cfg2's
+// paired N = 2 plan stays (split: 0.999 -> 1.126).  The env var (or macro)
+// DTA_FWD_BSPLIT = 0 / 1 forces it off / on.
+#ifndef DTA_FWD_BSPLIT
+#define DTA_FWD_BSPLIT -1
+#endif
+static inline int fwd_bsplit_env() {
+  static const int v = [] {
+    const char* s = getenv("DTA_FWD_BSPLIT");
+    return s && *s ? atoi(s) : DTA_FWD_BSPLIT;
+  }();
+  return v;
+}
+
 template <class E, int HS, int N, int DV_ = 2 * HS>
 struct Plan {
   static constexpr int DV = DV_;
@@ -1936,7 +1990,22 @@ int launch_fwd_t(const FwdParams& p, hipStream_t st) {
   constexpr int DVC = FP::DVC, NW = FP::NW;
   constexpr int QH = FP::QH;
   constexpr int bytes = FwdCfg<E, HS, N, DVC, NW, FP::QREG, QH>::bytes;
-  dim3 grid((p.T + NW * 32 - 1) / (NW * 32), p.H * (PL::DV / DVC), p.B);
+  if constexpr (N >= 2 && Plan<E, HS, 1, PL::DV>::ok) {
+    // auto: the N-branch plan splits dv, or (16-bit, head size >= 64) it is not the
+    // paired two-workgroups-per-CU plan (N >= 3, head size 96 / 128: one wave per SIMD)
+    constexpr bool AUTO = DVC < PL::DV || (sizeof(E) == 2 && HS >= 64 && !FwdPick<E, HS, N, PL::DV>::pair);
+    const int env = fwd_bsplit_env();
+    if (env > 0 || (env < 0 && AUTO)) {
+      FwdParams q = p;
+      q.bsplit = N;
+      if (int e = launch_fwd_t<E, HS, 1, DV_, DROP>(q, st)) return e;
+      const int64_t n = (int64_t)p.B * p.T * p.H * (PL::DV / (16 / (int)sizeof(E)));
+      hipLaunchKernelGGL((branch_combine_kernel<E, N>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, p);
+      return (int)hipGetLastError();
+    }
+  }
+  const int nsp = (N == 1 && p.bsplit > 1) ? p.bsplit : 1;
+  dim3 grid((p.T + NW * 32 - 1) / (NW * 32), p.H * nsp * (PL::DV / DVC), p.B);
   auto run = [&](auto SRDV) -> int {
     auto kern = attn_fwd_kernel<E, HS, N, DVC, NW, FP::QREG, decltype(SRDV)::value, DROP, QH>;
     if (int e = set_smem(kern, bytes)) return e;

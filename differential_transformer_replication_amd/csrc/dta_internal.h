@@ -21,6 +21,8 @@ struct FwdParams {
   uint32_t drop_thr;   // attention dropout: keep iff hash >= drop_thr (= p * 2^32); 0 = off
   float drop_scale;    // 1 / (1 - p)
   uint32_t drop_seed_lo, drop_seed_hi;
+  int bsplit;          // launcher-internal: > 1 = branch-split launch of the N = 1 kernel
+                       // (one branch of bsplit per workgroup; writes O_i and LSE_i only)
 };
 
 struct BwdParams {
