@@ -76,6 +76,8 @@ DROP_CASES = [  # H, N, hs, T, dv, rope, p
     (2, 2, 64, 129, 128, False, 0.1), (1, 3, 32, 200, 64, True, 0.3), (2, 4, 32, 97, 64, True, 0.1),
     (2, 2, 128, 130, 256, False, 0.5), (2, 1, 64, 150, 64, True, 0.1),     # the control model's N=1, dv=hs
     (1, 2, 64, 700, 128, False, 0.2),
+    # branch-split forward (one branch per workgroup + combine) with the mask: N = 3 / 4 at hs = 64
+    (2, 3, 64, 150, 128, True, 0.2), (1, 4, 64, 100, 128, False, 0.1),
 ]
 
 

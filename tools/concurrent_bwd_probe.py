@@ -1,0 +1,121 @@
+"""Probe: what would running the dQ and dK/dV kernels concurrently (two streams) buy?
+
+The dK/dV kernel reads the delta rows the dQ kernel's prologue writes, so a real
+concurrent backward needs those rows first (a separate delta pass).  This probe skips
+that pass: after one full backward the delta workspace already holds the rows of these
+exact inputs, and the dQ launch rewrites the same values while dK/dV reads them.  It
+times, interleaved in one process:
+  serial     pre + dq + dkdv on one stream
+  concurrent pre + dq on stream A, dkdv on stream B (forked after pre), joined
+and checks that the concurrent pass leaves dqkv bitwise equal to the serial one.
+
+    python tools/concurrent_bwd_probe.py [--shape B,H,hs,N,T] [--rounds 6] [--reps 6]
+"""
+import argparse
+import ctypes
+import json
+import math
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from differential_transformer_replication_amd import _lib  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shape", default="8,16,64,2,4096")
+    ap.add_argument("--rounds", type=int, default=6)
+    ap.add_argument("--reps", type=int, default=6)
+    args = ap.parse_args()
+    B, H, hs, N, T = (int(x) for x in args.shape.split(","))
+    dv = 2 * hs
+    dev = torch.device("cuda", 0)
+    lib = ctypes.CDLL(os.path.join(ROOT, "differential_transformer_replication_amd", "lib", "libdiffattn.so"))
+    P = ctypes.POINTER
+    lib.dta_attn_fwd.argtypes = [P(_lib.AttnFwdArgs), ctypes.c_void_p]
+    lib.dta_attn_bwd.argtypes = [P(_lib.AttnBwdArgs), ctypes.c_void_p]
+    g = torch.Generator(device=dev).manual_seed(0)
+    W = 2 * H * N * hs + H * dv
+    nq = H * N * hs
+    qkv = torch.randn(B, T, W, device=dev, generator=g).to(torch.bfloat16)
+    do = torch.randn(B, T, H, dv, device=dev, generator=g).to(torch.bfloat16)
+    coef = torch.randn(H, N, device=dev, generator=g) * 0.5
+    coef[:, 0] = 1.0
+    q = qkv[..., :nq].unflatten(-1, (H, N, hs))
+    k = qkv[..., nq:2 * nq].unflatten(-1, (H, N, hs))
+    v = qkv[..., 2 * nq:].unflatten(-1, (H, dv))
+    o = torch.empty(B, T, H, dv, device=dev, dtype=torch.bfloat16)
+    obr = torch.empty(N, B, T, H, dv, device=dev, dtype=torch.bfloat16)
+    lse = torch.empty(N, B, H, T, device=dev)
+    dqkv = torch.zeros_like(qkv)
+    dcoef = torch.empty(H, N, device=dev)
+    delta = torch.empty(N, B, H, T, device=dev)
+    obr_t = _lib.DtaTensor(obr.data_ptr(), *obr.stride()[1:4], obr.stride(0))
+    scale = 1.0 / math.sqrt(hs)
+    fa = _lib.AttnFwdArgs(0, B, T, H, N, hs, dv, scale, 0.0, _lib.tensor5(q), _lib.tensor5(k), _lib.tensor5(v),
+                          _lib.tensor5(o), obr_t, lse.data_ptr(), coef.data_ptr())
+    dq = dqkv[..., :nq].unflatten(-1, (H, N, hs))
+    dk = dqkv[..., nq:2 * nq].unflatten(-1, (H, N, hs))
+    dvv = dqkv[..., 2 * nq:].unflatten(-1, (H, dv))
+    ba = _lib.AttnBwdArgs(0, B, T, H, N, hs, dv, scale, 0.0, _lib.tensor5(q), _lib.tensor5(k), _lib.tensor5(v),
+                          obr_t, lse.data_ptr(), coef.data_ptr(), _lib.tensor5(do), _lib.tensor5(dq),
+                          _lib.tensor5(dk), _lib.tensor5(dvv), dcoef.data_ptr(), delta.data_ptr(), None,
+                          _lib.BWD_PRE, None)
+    sa = torch.cuda.Stream(dev)
+    sb = torch.cuda.Stream(dev)
+
+    def bwd(stream, stages):
+        ba.stages = stages
+        rc = lib.dta_attn_bwd(ba, stream.cuda_stream)
+        if rc:
+            raise RuntimeError(f"bwd rc {rc}")
+
+    def serial():
+        bwd(sa, _lib.BWD_PRE)
+        bwd(sa, _lib.BWD_DQ)
+        bwd(sa, _lib.BWD_DKDV)
+
+    def concurrent():
+        bwd(sa, _lib.BWD_PRE)
+        e = torch.cuda.Event()
+        e.record(sa)
+        sb.wait_event(e)
+        bwd(sa, _lib.BWD_DQ)
+        bwd(sb, _lib.BWD_DKDV)
+        j = torch.cuda.Event()
+        j.record(sb)
+        sa.wait_event(j)
+
+    with torch.cuda.stream(sa):
+        if lib.dta_attn_fwd(fa, sa.cuda_stream):
+            raise RuntimeError("fwd")
+    serial()
+    torch.cuda.synchronize()
+    ref = dqkv.clone()
+    concurrent()
+    torch.cuda.synchronize()
+    same = bool(torch.equal(ref, dqkv))
+    res = {"serial": [], "concurrent": []}
+    for r in range(args.rounds):
+        for name, fn in (("serial", serial), ("concurrent", concurrent))[::(1 if r % 2 == 0 else -1)]:
+            fn()
+            ev = []
+            for _ in range(args.reps):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(sa)
+                fn()
+                e1.record(sa)
+                ev.append((e0, e1))
+            torch.cuda.synchronize()
+            res[name].extend(a.elapsed_time(b) for a, b in ev)
+    med = {k: round(sorted(x)[len(x) // 2], 4) for k, x in res.items()}
+    print(json.dumps({"shape": dict(B=B, H=H, hs=hs, N=N, T=T), "median_ms": med,
+                      "min_ms": {k: round(min(x), 4) for k, x in res.items()}, "dqkv_bitwise_equal": same}))
+
+
+if __name__ == "__main__":
+    main()
