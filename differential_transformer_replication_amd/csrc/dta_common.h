@@ -62,10 +62,33 @@ __device__ __forceinline__ int xcd_remap(int id, int n) {
 #ifndef DTA_LPT
 #define DTA_LPT 1
 #endif
+// DTA_LPT_GROUP = G > 0 (default 4): each XCD walks its (y, z) pairs G at a time,
+// longest-first inside a group, so only about 2G pairs' K/V (forward, dQ) or Q/dO
+// (dK/dV) are live in that XCD's L2 at once instead of all of them (needs gridDim.y *
+// gridDim.z % 8 == 0; blocks are dealt to XCD id % 8).  One-process A/B at cfg2
+// (profiles/r03_lpt_group_ab.json): fwd+dq+dkdv 3.052 -> 2.891 ms (G = 1 / 2 / 3 / 6 / 8:
+// 3.140 / 3.001 / 3.081 / 2.926 / 2.912); fabric reads per launch fwd 2575 -> 734 MB,
+// dq 2929 -> 1258, dK/dV 3146 -> 867; cfg3 N=3 1.231 -> 1.211, cfg5 unchanged.  0 = the
+// ungrouped longest-first order.
+#ifndef DTA_LPT_GROUP
+#define DTA_LPT_GROUP 4
+#endif
 __device__ __forceinline__ void lpt_order(int& r, int& y, int& z, int& id) {
   id = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  const int nyz = gridDim.y * gridDim.z;
+  if (DTA_LPT && DTA_LPT_GROUP > 0 && nyz % 8 == 0) {
+    const int xcd = id & 7, s = id >> 3;            // s-th block this XCD receives
+    const int per = nyz >> 3, R = gridDim.x;        // pairs per XCD, work ranks
+    const int g = s / (R * DTA_LPT_GROUP);
+    const int gsz = min(DTA_LPT_GROUP, per - g * DTA_LPT_GROUP);
+    const int t = s - g * R * DTA_LPT_GROUP;
+    r = t / gsz;
+    const int pair = xcd + 8 * (g * DTA_LPT_GROUP + t % gsz);
+    y = pair % gridDim.y;
+    z = pair / gridDim.y;
+    return;
+  }
   if (DTA_LPT) {
-    const int nyz = gridDim.y * gridDim.z;
     r = id / nyz;
     const int rest = id - r * nyz;
     y = rest % gridDim.y;
