@@ -548,6 +548,9 @@ inline bool kv_layout_ok(const P& p, int es) {
 #ifndef DTA_FWD_PIPE
 #define DTA_FWD_PIPE 3
 #endif
+#ifndef DTA_FWD_FAST
+#define DTA_FWD_FAST 1
+#endif
 #ifndef DTA_DKDV_FUSE1
 #define DTA_DKDV_FUSE1 1
 #endif
@@ -711,25 +714,21 @@ void attn_fwd_kernel(FwdParams p) {
   };
   const int tile_pieces = SRD ? KR::pieces(wave)
                               : N * stage_pieces<E, HSP, BN, HS, NW>(wave) + stage_pieces<E, DVP, BN, DVC, NW>(wave);
-  for (int j = 0; j < NS - 1; ++j)
-    if (j < ntiles) stage_kv(j, j);
-  wait_vm(tile_pieces * max(0, min(NS - 1, ntiles) - 1));   // tile 0 (and the Q block) landed
-  lds_barrier();
-
   f32x16 acc[N][NDB];
   float m[N], l[N];
-#pragma unroll
-  for (int i = 0; i < N; ++i) {
-    m[i] = -INFINITY;
-    l[i] = 0.f;
-#pragma unroll
-    for (int d = 0; d < NDB; ++d) acc[i][d] = f32x16{};
-  }
   const bool wave_live = qw0 < T;
+  // FAST (16-bit, no dropout): after a workgroup's first key tile the reference m stays
+  // fixed -- no per-tile row maximum, no rescale: P = exp2(S sl2 - m) straight off the
+  // QK^T accumulators.  A lane whose partial row sum leaves [0, 2^60] (a row maximum that
+  // grew by ~55 log2 units past its first tile's, or a non-finite score) marks the
+  // workgroup, which then re-runs its whole key loop on the per-tile-maximum path.
+  // (N <= 2 plans with two waves per SIMD: the one-wave 512-register plans and the hs = 32
+  // N = 3 paired plan spill with it)
+  constexpr bool FAST = DTA_FWD_FAST && sizeof(E) == 2 && !DROP && N <= 2 && (CF::PAIR || CF::WPE >= 2);
+  float bad = 0.f;
 
   // per-lane LDS read bases kept in registers across the loop (see attn_dkdv_kernel)
-  int LrK = 0, LtV = 0;
-  if constexpr (sizeof(E) == 2) { LrK = row_lane<KI::ROWB>(lane); LtV = tr_lane<VI::ROWB>(lane); }
+  int LrK = 0, LtV = 0;      // set per attempt, after the ring prologue
   // key = k0 + kb*32 + rowof(r); masked when key > qrow or key >= T
   auto mask_scores = [&](int k0, f32x16 (&sa)[NKB]) {
     const int lim = min(qrow, T - 1) - k0 - 4 * hf;
@@ -752,7 +751,7 @@ void attn_fwd_kernel(FwdParams p) {
   };
   // P = exp2(S * scale*log2e - m), row sums (two chains), packed to the PV operand;
   // with dropout the row sum keeps every element and the PV operand only the kept ones
-  auto exp_pack = [&](int i, int k0, f32x16 (&sa)[NKB], frag (&pf)[NKB * SPB]) {
+  auto exp_pack = [&](int i, int k0, f32x16 (&sa)[NKB], frag (&pf)[NKB * SPB]) -> float {
     const float mi = m[i];
     float ls0 = 0.f, ls1 = 0.f;
 #pragma unroll
@@ -766,7 +765,8 @@ void attn_fwd_kernel(FwdParams p) {
         ls0 += e0;
         ls1 += e1;
       }
-    l[i] += ls0 + ls1;
+    const float ls = ls0 + ls1;
+    l[i] += ls;
     if constexpr (DROP) {
       const uint32_t key = drop_key(p.drop_seed_lo, p.drop_seed_hi, b, hh, br + i, p.H, nsp > 1 ? nsp : N);
 #pragma unroll
@@ -785,10 +785,19 @@ void attn_fwd_kernel(FwdParams p) {
         for (int s = 0; s < 16; ++s) pf[kb * SPB + s] = sa[kb][s];
       }
     }
+    return ls;
   };
-  // one branch's mask, max, deferred rescale (only when some row's max grew by > 2^THR), exp
-  auto softmax_branch = [&](int i, int k0, auto MASKED, f32x16 (&sa)[NKB], frag (&pf)[NKB * SPB]) {
+  // one branch's mask, max, deferred rescale (only when some row's max grew by > 2^THR), exp;
+  // fast: exp against the fixed m, the lane's partial sum checked instead
+  auto softmax_branch = [&](int i, int k0, auto MASKED, f32x16 (&sa)[NKB], frag (&pf)[NKB * SPB], auto FASTT) {
     if constexpr (decltype(MASKED)::value) mask_scores(k0, sa);
+    if constexpr (decltype(FASTT)::value) {
+      {
+        const float ls = exp_pack(i, k0, sa, pf);
+        bad = (ls <= 0x1p60f) ? bad : 1.f;      // NaN / inf / huge: re-run
+        return;
+      }
+    }
     const float mx = wave_max_halves(row_max(sa)) * p.sl2;
     if (__any(mx > m[i] + THR)) {
       const float mnew = fmaxf(m[i], mx);
@@ -801,7 +810,7 @@ void attn_fwd_kernel(FwdParams p) {
     exp_pack(i, k0, sa, pf);
   };
   // QK^T + online softmax of one key tile for every branch, P packed as the PV B operand
-  auto phase_a = [&](int kt, auto MASKED, frag (&pf)[N][NKB * SPB]) {
+  auto phase_a = [&](int kt, auto MASKED, frag (&pf)[N][NKB * SPB], auto FASTT) {
     constexpr bool MASK = decltype(MASKED)::value;
     const int buf = kt % NS;
     const int k0 = kt * BN;
@@ -873,7 +882,7 @@ void attn_fwd_kernel(FwdParams p) {
           }
         }
       }
-      softmax_branch(i, k0, MASKED, sa[i], pf[i]);
+      softmax_branch(i, k0, MASKED, sa[i], pf[i], FASTT);
     }
   };
   // O_i^T += V^T P_i^T, one V fragment feeds every branch
@@ -940,7 +949,7 @@ void attn_fwd_kernel(FwdParams p) {
   // query row and inside T need no mask; the block's diagonal / tail tiles do
   // (one loop body with both variants behind a branch spills)
   Stamps st;
-  auto step = [&](int kt, auto MASKED) {
+  auto step = [&](int kt, auto MASKED, auto FASTT) {
     // keep lane-derived addresses loop-variant: recomputed per tile instead of
     // hoisted into (spilled) registers across the whole loop
     asm volatile("" : "+v"(lane));
@@ -953,7 +962,7 @@ void attn_fwd_kernel(FwdParams p) {
     st.lap<0>();
     if (live) {
       frag pf[N][NKB * SPB];
-      phase_a(kt, MASKED, pf);
+      phase_a(kt, MASKED, pf, FASTT);
       st.lap<1>();
       phase_b(kt, pf);
       st.lap<2>();
@@ -964,10 +973,48 @@ void attn_fwd_kernel(FwdParams p) {
     lds_barrier();
     st.lap<4>();
   };
-  st.start();
-  const int nfull = min(ntiles, min((q0 + 1) / BN, T / BN));
-  for (int kt = 0; kt < nfull; ++kt) step(kt, std::false_type{});
-  for (int kt = nfull; kt < ntiles; ++kt) step(kt, std::true_type{});
+  // one pass over the key tiles: ring prologue, state reset, the unmasked then the masked
+  // loop; with FAST every tile after the first runs without the per-tile maximum
+  auto attempt = [&](bool safe) {
+    for (int j = 0; j < NS - 1; ++j)
+      if (j < ntiles) stage_kv(j, j);
+    wait_vm(tile_pieces * max(0, min(NS - 1, ntiles) - 1));   // tile 0 (and the Q block) landed
+    lds_barrier();
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      m[i] = -INFINITY;
+      l[i] = 0.f;
+#pragma unroll
+      for (int d = 0; d < NDB; ++d) acc[i][d] = f32x16{};
+    }
+    if constexpr (sizeof(E) == 2) { LrK = row_lane<KI::ROWB>(lane); LtV = tr_lane<VI::ROWB>(lane); }
+    st.start();
+    const int nfull = min(ntiles, min((q0 + 1) / BN, T / BN));
+    // per-tile-maximum tiles: all of them (safe, or no FAST), else the first one only
+    const int kslow = (safe || !FAST) ? ntiles : min(1, ntiles);
+    for (int kt = 0; kt < min(nfull, kslow); ++kt) step(kt, std::false_type{}, std::false_type{});
+    for (int kt = nfull; kt < kslow; ++kt) step(kt, std::true_type{}, std::false_type{});
+    if constexpr (FAST) {
+      for (int kt = kslow; kt < nfull; ++kt) step(kt, std::false_type{}, std::true_type{});
+      for (int kt = max(kslow, nfull); kt < ntiles; ++kt) step(kt, std::true_type{}, std::true_type{});
+    }
+  };
+  // one inlined copy of the loops: pass 1 (FAST) re-runs only a flagged workgroup
+  for (int pass = 0; pass < (FAST ? 2 : 1); ++pass) {
+    attempt(pass == 1);
+    if constexpr (!FAST) break;
+    if (pass == 1) break;
+    // rows past T never count; the ring is idle (the last step drained it behind a barrier)
+    int* flag = reinterpret_cast<int*>(Kb);
+    const bool mine = __any(wave_live && qrow < T && bad != 0.f);
+    if (lane == 0) flag[wave] = mine ? 1 : 0;
+    lds_barrier();
+    bool any = false;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) any |= flag[w] != 0;
+    lds_barrier();
+    if (!any) break;
+  }
   st.lap<5>();
   st.flush(p.stamps, lin * NW + wave, lane);
 
@@ -1959,8 +2006,8 @@ __global__ __launch_bounds__(256) void branch_combine_kernel(FwdParams p) {
 // softmax: head size 128 at N = 2, cfg5; N = 4 at head size 64, cfg3) or runs one wave
 // per SIMD (N = 3 at head size 64, cfg3).  One-process A/B (profiles/r03_bsplit_ab.json):
 // cfg5 fwd 20.54 -> 12.66 ms, cfg3 N=4 0.744 -> 0.485, N=3 0.409 -> 0.361; cfg2's
-// paired N = 2 plan stays (split: 0.999 -> 1.126).  The env var (or macro)
-// DTA_FWD_BSPLIT = 0 / 1 forces it off / on.
+// paired N = 2 plan stays (split: 0.999 -> 1.126).  The macro DTA_FWD_BSPLIT = 0 builds
+// no split at all; the env var DTA_FWD_BSPLIT = 1 also splits the non-auto plans.
 #ifndef DTA_FWD_BSPLIT
 #define DTA_FWD_BSPLIT -1
 #endif
@@ -1990,12 +2037,15 @@ int launch_fwd_t(const FwdParams& p, hipStream_t st) {
   constexpr int DVC = FP::DVC, NW = FP::NW;
   constexpr int QH = FP::QH;
   constexpr int bytes = FwdCfg<E, HS, N, DVC, NW, FP::QREG, QH>::bytes;
-  if constexpr (N >= 2 && Plan<E, HS, 1, PL::DV>::ok) {
-    // auto: the N-branch plan splits dv, or (16-bit, head size >= 64) it is not the
-    // paired two-workgroups-per-CU plan (N >= 3, head size 96 / 128: one wave per SIMD)
-    constexpr bool AUTO = DVC < PL::DV || (sizeof(E) == 2 && HS >= 64 && !FwdPick<E, HS, N, PL::DV>::pair);
-    const int env = fwd_bsplit_env();
-    if (env > 0 || (env < 0 && AUTO)) {
+  // auto: the N-branch plan splits dv, or (16-bit, head size >= 64) it is not the paired
+  // two-workgroups-per-CU plan (N >= 3, head size 96 / 128: one wave per SIMD).  Auto
+  // plans always split (their N-branch kernel is not built); DTA_FWD_BSPLIT = 1 also
+  // splits the others.
+  constexpr bool CAN = N >= 2 && Plan<E, HS, 1, PL::DV>::ok;
+  constexpr bool AUTO = CAN && DTA_FWD_BSPLIT != 0 &&
+                        (DVC < PL::DV || (sizeof(E) == 2 && HS >= 64 && !FwdPick<E, HS, N, PL::DV>::pair));
+  if constexpr (CAN) {
+    if (AUTO || fwd_bsplit_env() > 0) {
       FwdParams q = p;
       q.bsplit = N;
       if (int e = launch_fwd_t<E, HS, 1, DV_, DROP>(q, st)) return e;
@@ -2004,6 +2054,9 @@ int launch_fwd_t(const FwdParams& p, hipStream_t st) {
       return (int)hipGetLastError();
     }
   }
+  if constexpr (AUTO) {
+    return -2;       // unreachable
+  } else {
   const int nsp = (N == 1 && p.bsplit > 1) ? p.bsplit : 1;
   dim3 grid((p.T + NW * 32 - 1) / (NW * 32), p.H * nsp * (PL::DV / DVC), p.B);
   auto run = [&](auto SRDV) -> int {
@@ -2019,6 +2072,7 @@ int launch_fwd_t(const FwdParams& p, hipStream_t st) {
     e = run(std::false_type{});
   if (e) return e;
   return (int)hipGetLastError();
+  }
 }
 
 template <class E, int HS, int N, int DV_, bool DROP>

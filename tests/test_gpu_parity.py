@@ -145,6 +145,33 @@ def test_forced_rescale(dtype):
     assert rel_err(cg.grad.cpu(), c64.grad) < tol, "dcoef"
 
 
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("jump", [30.0, 200.0, 4000.0])
+def test_forward_max_growth(dtype, jump):
+    """The 16-bit forward keeps each row's reference maximum fixed after the first key
+    tile (no per-tile maximum) and re-runs a workgroup on the per-tile-maximum path
+    when a row's maximum grows too far.  jump 30: +~10 log2 units (fixed-reference path);
+    200: +~70 (re-run); 4000: the exponent overflows fp32 (re-run).  Forward output
+    against the fp64 oracle; every row finite."""
+    ops = _ops()
+    H, N, hs, T, B = 2, 2, 64, 900, 1
+    g = torch.Generator().manual_seed(11)
+    W = ops.packed_width(H, N, hs, 2 * hs)
+    nq = H * N * hs
+    qkv = torch.randn(B, T, W, generator=g) * 0.3
+    u = torch.ones(hs) / math.sqrt(hs)
+    q = qkv[..., :nq].view(B, T, H, N, hs)
+    k = qkv[..., nq:2 * nq].view(B, T, H, N, hs)
+    q[:, :, :, 0] += 2.0 * u
+    k[:, 700, :, 0] = jump * u
+    coef = torch.tensor([[1.0, -0.4], [1.0, -0.6]])
+    x64 = qkv.to(dtype).double()
+    ref = _oracle_core(x64, coef.double(), H, N, hs)
+    out = ops.diff_attention(qkv.to(dtype).to(DEV), coef.to(DEV), H, N, hs).float().cpu()
+    assert torch.isfinite(out).all()
+    assert rel_err(out, ref) < TOL[dtype]
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("C", [48, 384, 2048, 4104])
 def test_group_ln_scale(dtype, C):
