@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get("DTA_LIB", os.path.join(_HERE, "lib", "libdiffattn.so"
 DTA_BF16, DTA_F16, DTA_F32 = 0, 1, 2
 _DTYPES = {torch.bfloat16: DTA_BF16, torch.float16: DTA_F16, torch.float32: DTA_F32}
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 # every symbol include/diffattn.h declares
 EXPORTS = ("dta_attn_fwd", "dta_attn_bwd", "dta_attn_bwd_workspace_bytes", "dta_attn_bwd_dcoef_partial_bytes",

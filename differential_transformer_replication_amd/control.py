@@ -8,7 +8,7 @@ their N=1 case (one branch, coefficient 1, value width dv = hs; SURVEY 8(f) item
 kernels' counter-based mask, include/diffattn.h).  Two cases keep PyTorch's
 ``scaled_dot_product_attention`` instead: CPU tensors (the control model is not
 the hot path and stays runnable on the host) and head sizes without a dv = hs
-plan (the fused plans cover 64 and 128).
+plan (head sizes above 128).
 """
 from __future__ import annotations
 
@@ -26,10 +26,11 @@ __all__ = ["precompute_freqs_cis", "apply_rotary_emb", "Head", "MultiHeadAttenti
 
 
 def _fused_ok(x: torch.Tensor, p: float, hs: int) -> bool:
-    # the fused kernels' standard-attention plans (dv = hs: head sizes 64, 96, 128);
+    # the fused kernels' standard-attention plans (dv = hs: head sizes 32, 64, 96, 128, and
+    # every other head size up to 128 zero-padded to one of them, ops.padded_head);
     # x.dtype is the projection's dtype under autocast too
     dt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else x.dtype
-    return x.is_cuda and 0.0 <= p < 1.0 and ops.supported(dt, hs, 1, hs)
+    return x.is_cuda and 0.0 <= p < 1.0 and ops.attention_supported(dt, hs, 1, hs)
 
 
 def _fused_attention(qkv: torch.Tensor, H: int, hs: int, freqs_cis: torch.Tensor, p: float = 0.0) -> torch.Tensor:

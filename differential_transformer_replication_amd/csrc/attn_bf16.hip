@@ -5,5 +5,5 @@ namespace dta {
 int launch_attn_fwd_bf16(const FwdParams& p, hipStream_t st) { return dispatch_fwd<__bf16, false>(p, st); }
 int launch_attn_dq_bf16(const BwdParams& p, hipStream_t st) { return dispatch_dq<__bf16, false>(p, st); }
 int launch_attn_dkdv_bf16(const BwdParams& p, hipStream_t st) { return dispatch_dkdv<__bf16, false>(p, st); }
-bool attn_supported_bf16(int hs, int n, int dv) { return supported_t<__bf16>(hs, n, dv); }
+bool attn_native_bf16(int hs, int n, int dv) { return native_t<__bf16>(hs, n, dv); }
 }  // namespace dta

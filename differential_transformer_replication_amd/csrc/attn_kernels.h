@@ -680,7 +680,7 @@ void attn_fwd_kernel(FwdParams p) {
 
   float coef[N];
 #pragma unroll
-  for (int i = 0; i < N; ++i) coef[i] = nsp > 1 ? 1.f : p.coef[hh * N + i];
+  for (int i = 0; i < N; ++i) coef[i] = nsp > 1 ? 1.f : p.coef[hh * p.cst + i];
 
   frag qf[NQR > 0 ? NQR : 1][NQR > 0 ? NSQ : 1];
 #pragma unroll
@@ -719,12 +719,16 @@ void attn_fwd_kernel(FwdParams p) {
   const bool wave_live = qw0 < T;
   // FAST (16-bit, no dropout): after a workgroup's first key tile the reference m stays
   // fixed -- no per-tile row maximum, no rescale: P = exp2(S sl2 - m) straight off the
-  // QK^T accumulators.  A lane whose partial row sum leaves [0, 2^60] (a row maximum that
-  // grew by ~55 log2 units past its first tile's, or a non-finite score) marks the
-  // workgroup, which then re-runs its whole key loop on the per-tile-maximum path.
+  // QK^T accumulators.  P may then exceed 1 by as much as the row maximum grew, and it is
+  // packed to E for the PV operand, so the bound is the operand type's range: a lane whose
+  // partial row sum (which bounds every P it packed) leaves [0, LSMAX] marks the workgroup,
+  // which then re-runs its whole key loop on the per-tile-maximum path.  bf16 shares fp32's
+  // exponent range: 2^60 (a row maximum that grew by ~55 log2 units past its first tile's,
+  // or a non-finite score); fp16 saturates at 65504: 2^15.
   // (N <= 2 plans with two waves per SIMD: the one-wave 512-register plans and the hs = 32
   // N = 3 paired plan spill with it)
   constexpr bool FAST = DTA_FWD_FAST && sizeof(E) == 2 && !DROP && N <= 2 && (CF::PAIR || CF::WPE >= 2);
+  constexpr float LSMAX = std::is_same<E, _Float16>::value ? 0x1p15f : 0x1p60f;
   float bad = 0.f;
 
   // per-lane LDS read bases kept in registers across the loop (see attn_dkdv_kernel)
@@ -794,7 +798,7 @@ void attn_fwd_kernel(FwdParams p) {
     if constexpr (decltype(FASTT)::value) {
       {
         const float ls = exp_pack(i, k0, sa, pf);
-        bad = (ls <= 0x1p60f) ? bad : 1.f;      // NaN / inf / huge: re-run
+        bad = (ls <= LSMAX) ? bad : 1.f;        // NaN / inf / past the operand range: re-run
         return;
       }
     }
@@ -1028,7 +1032,9 @@ void attn_fwd_kernel(FwdParams p) {
       p.lse[(((int64_t)(br + i) * p.B + b) * p.H + hh) * T + qrow] = -(m[i] + __builtin_log2f(lt));   // stored negated
   }
   E* go = reinterpret_cast<E*>(p.o.p) + b * p.o.sb + (int64_t)qrow * p.o.st + hh * p.o.sh + dc0;
-  E* gob = reinterpret_cast<E*>(p.obr.p) + b * p.obr.sb + (int64_t)qrow * p.obr.st + hh * p.obr.sh + br * p.obr.si + dc0;
+  // O_i stays fp32 (saved for the backward's delta_i = <dO, O_i>, whose sums feed d(lambda))
+  float* gob = reinterpret_cast<float*>(p.obr.p) + b * p.obr.sb + (int64_t)qrow * p.obr.st + hh * p.obr.sh +
+               br * p.obr.si + dc0;
 #pragma unroll
   for (int d = 0; d < NDB; ++d)
 #pragma unroll
@@ -1039,7 +1045,7 @@ void attn_fwd_kernel(FwdParams p) {
       for (int i = 0; i < N; ++i) {
         const float a0 = acc[i][d][4 * g + 0] * inv[i], a1 = acc[i][d][4 * g + 1] * inv[i];
         const float a2 = acc[i][d][4 * g + 2] * inv[i], a3 = acc[i][d][4 * g + 3] * inv[i];
-        store4<E>(gob + i * p.obr.si + e, a0, a1, a2, a3);
+        store4<float>(gob + i * p.obr.si + e, a0, a1, a2, a3);
         o0 = fmaf(coef[i], a0, o0); o1 = fmaf(coef[i], a1, o1);
         o2 = fmaf(coef[i], a2, o2); o3 = fmaf(coef[i], a3, o3);
       }
@@ -1124,7 +1130,7 @@ void attn_dq_kernel(BwdParams p) {
   const E* gk = reinterpret_cast<const E*>(p.k.p) + b * p.k.sb + hh * p.k.sh;
   const E* gv = reinterpret_cast<const E*>(p.v.p) + b * p.v.sb + hh * p.v.sh;
   const E* gdo = reinterpret_cast<const E*>(p.dout.p) + b * p.dout.sb + hh * p.dout.sh;
-  const E* gob = reinterpret_cast<const E*>(p.obr.p) + b * p.obr.sb + hh * p.obr.sh;
+  const float* gob = reinterpret_cast<const float*>(p.obr.p) + b * p.obr.sb + hh * p.obr.sh;   // fp32 O_i
 
   const int kend = min(T, q0 + BM);
   const int ntiles = (kend + BN - 1) / BN;
@@ -1159,7 +1165,7 @@ void attn_dq_kernel(BwdParams p) {
     df[s] = rowok ? O::load_global(gdo + (int64_t)qrow * p.dout.st + s * KS + hf * O::KH) : O::zero();
 #pragma unroll
   for (int i = 0; i < N; ++i) {
-    coef[i] = p.coef[hh * N + i];
+    coef[i] = p.coef[hh * p.cst + i];
     if (i < NQR) {
 #pragma unroll
       for (int s = 0; s < NSQ; ++s)
@@ -1178,12 +1184,15 @@ void attn_dq_kernel(BwdParams p) {
     if (rowok) {
 #pragma unroll
       for (int s = 0; s < NSV; ++s) {
-        const frag o = O::load_global(gob + (int64_t)qrow * p.obr.st + i * p.obr.si + s * KS + hf * O::KH);
+        const float* o = gob + (int64_t)qrow * p.obr.st + i * p.obr.si + s * KS + hf * O::KH;
         if constexpr (sizeof(E) == 2) {
+          const f32x4 o0 = *reinterpret_cast<const f32x4*>(o), o1 = *reinterpret_cast<const f32x4*>(o + 4);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) d = fmaf((float)df[s][j], (float)o[j], d);
+          for (int j = 0; j < 4; ++j) d = fmaf((float)df[s][j], o0[j], d);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) d = fmaf((float)df[s][4 + j], o1[j], d);
         } else {
-          d = fmaf(df[s], o, d);
+          d = fmaf(df[s], *o, d);
         }
       }
     }
@@ -1199,9 +1208,9 @@ void attn_dq_kernel(BwdParams p) {
     for (int o = 32; o > 0; o >>= 1) w += __shfl_xor(w, o, 64);
     if (p.dcoef_part) {
       // one slot per (h, i, b, 32-row block): every slot written once, summed in order later
-      if (lane == 0 && qw0 < T) p.dcoef_part[(((int64_t)hh * N + i) * p.B + b) * ((T + 31) / 32) + qw0 / 32] = w;
+      if (lane == 0 && qw0 < T) p.dcoef_part[(((int64_t)hh * p.cst + i) * p.B + b) * ((T + 31) / 32) + qw0 / 32] = w;
     } else if (lane == 0 && qw0 < T) {
-      atomicAdd(p.dcoef + hh * N + i, w);
+      atomicAdd(p.dcoef + hh * p.cst + i, w);
     }
   }
 
@@ -1384,7 +1393,7 @@ void attn_dq_kernel(BwdParams p) {
               }
           } else {
           uint32_t dkey = 0;
-          if constexpr (DROP) dkey = drop_key(p.drop_seed_lo, p.drop_seed_hi, b, hh, i, p.H, N);
+          if constexpr (DROP) dkey = drop_key(p.drop_seed_lo, p.drop_seed_hi, b, hh, p.br0 + i, p.H, p.cst);
 #pragma unroll
           for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
@@ -1449,7 +1458,7 @@ void attn_dq_kernel(BwdParams p) {
         float a2 = dq[i][d][4 * g + 2] * sc, a3 = dq[i][d][4 * g + 3] * sc;
         if (p.rope) rope_inv4(p.rope, qrow, HS, e, a0, a1, a2, a3);
         if constexpr (OUTF32) {
-          store4<float>(p.dq32 + ((((int64_t)b * T + qrow) * p.H + hh) * N + i) * HS + e, a0, a1, a2, a3);
+          store4<float>(p.dq32 + ((((int64_t)b * T + qrow) * p.H + hh) * p.cst + i) * HS + e, a0, a1, a2, a3);
         } else {
           E* gdq = reinterpret_cast<E*>(p.dq.p) + b * p.dq.sb + (int64_t)qrow * p.dq.st + hh * p.dq.sh + i * p.dq.si;
           store4<E>(gdq + e, a0, a1, a2, a3);
@@ -1658,8 +1667,8 @@ void attn_dkdv_kernel(BwdParams p) {
   uint32_t dkey[N];
 #pragma unroll
   for (int i = 0; i < N; ++i) {
-    coef[i] = p.coef[hh * N + i];
-    dkey[i] = DROP ? drop_key(p.drop_seed_lo, p.drop_seed_hi, b, hh, i, p.H, N) : 0u;
+    coef[i] = p.coef[hh * p.cst + i];
+    dkey[i] = DROP ? drop_key(p.drop_seed_lo, p.drop_seed_hi, b, hh, p.br0 + i, p.H, p.cst) : 0u;
   }
   // this wave's key rows of every K_i and of V as B fragments
   // this wave's V rows as B fragments of dP = dO V^T (registers); K_i rows live in LDS
@@ -1956,7 +1965,11 @@ void attn_dkdv_kernel(BwdParams p) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int e = d * 32 + 8 * g + 4 * hf;
-        store4<E>(gdv + e, dv[d][4 * g], dv[d][4 * g + 1], dv[d][4 * g + 2], dv[d][4 * g + 3]);
+        float a0 = dv[d][4 * g], a1 = dv[d][4 * g + 1], a2 = dv[d][4 * g + 2], a3 = dv[d][4 * g + 3];
+        if (p.dv_acc) {        // a later branch group: dV = sum over every group's branches
+          a0 += (float)gdv[e]; a1 += (float)gdv[e + 1]; a2 += (float)gdv[e + 2]; a3 += (float)gdv[e + 3];
+        }
+        store4<E>(gdv + e, a0, a1, a2, a3);
       }
   }
 }
@@ -1971,8 +1984,11 @@ static inline int set_smem(K kernel, int bytes) {
 
 // O = sum_i c_i O_i after a branch-split forward (HBM-bound: N + 1 passes of
 // B*T*H*dv elements).  One thread per 16 bytes of an output row, fp32 sums.
-template <class E, int N>
+// NC > 0: the branch count at compile time; 0: p.N at run time (branch counts without
+// an N-branch plan, which always run branch-split).
+template <class E, int NC>
 __global__ __launch_bounds__(256) void branch_combine_kernel(FwdParams p) {
+  const int N = NC > 0 ? NC : p.N;
   constexpr int V = 16 / (int)sizeof(E);
   typedef float f32xv __attribute__((ext_vector_type(V)));
   typedef E ev __attribute__((ext_vector_type(V)));
@@ -1985,14 +2001,14 @@ __global__ __launch_bounds__(256) void branch_combine_kernel(FwdParams p) {
   const int hh = (int)(row % p.H);
   const int64_t bt = row / p.H;
   const int t = (int)(bt % p.T), b = (int)(bt / p.T);
-  const E* src = reinterpret_cast<const E*>(p.obr.p) + b * p.obr.sb + (int64_t)t * p.obr.st + hh * p.obr.sh + e;
+  const float* src = reinterpret_cast<const float*>(p.obr.p) + b * p.obr.sb + (int64_t)t * p.obr.st + hh * p.obr.sh + e;
   f32xv acc = f32xv{};
 #pragma unroll
   for (int i = 0; i < N; ++i) {
-    const ev x = *reinterpret_cast<const ev*>(src + i * p.obr.si);
-    const float c = p.coef[hh * N + i];
+    const f32xv x = *reinterpret_cast<const f32xv*>(src + i * p.obr.si);     // fp32 O_i
+    const float c = p.coef[hh * p.cst + i];
 #pragma unroll
-    for (int j = 0; j < V; ++j) acc[j] = fmaf(c, (float)x[j], acc[j]);
+    for (int j = 0; j < V; ++j) acc[j] = fmaf(c, x[j], acc[j]);
   }
   ev y;
 #pragma unroll
@@ -2150,19 +2166,51 @@ int launch_dkdv_t(const BwdParams& p, hipStream_t st) {
 #define DTA_FOR_CONFIGS(X) \
   X(16, 1, 32) X(16, 2, 32) X(16, 3, 32) X(16, 4, 32) X(32, 1, 64) X(32, 2, 64) X(32, 3, 64) X(32, 4, 64) \
   X(64, 1, 128) X(64, 2, 128) X(64, 3, 128) X(64, 4, 128) X(128, 1, 256) X(128, 2, 256) X(128, 3, 256) \
-  X(128, 4, 256) X(64, 1, 64) X(128, 1, 128) \
+  X(128, 4, 256) X(64, 1, 64) X(128, 1, 128) X(32, 1, 32) \
   X(96, 1, 192) X(96, 2, 192) X(96, 3, 192) X(96, 4, 192) X(96, 1, 96)
+
+// whether the N-branch plan of (HS, N, DV) is built for E
+template <class E>
+bool native_t(int hs, int n, int dv) {
+#define DTA_S(HS_, N_, DV_) if (hs == HS_ && n == N_ && dv == DV_) return Plan<E, HS_, N_, DV_>::ok;
+  DTA_FOR_CONFIGS(DTA_S)
+#undef DTA_S
+  return false;
+}
+
+// Any branch count N >= 2 whose N-branch plan is not built (N >= 5, fp32 N = 3 / 4 at head
+// sizes 96 / 128): N single-branch workgroups per (query block, head) -- the N = 1 kernel
+// with bsplit = N, each writing its O_i and LSE_i -- then the combine O = sum_i c_i O_i
+// with the branch count at run time.  The backward runs such calls as branch groups
+// (capi.hip).
+template <class E, bool DROP>
+int fwd_branch_split_any(const FwdParams& p, hipStream_t st) {
+  FwdParams q = p;
+  q.bsplit = p.N;
+  int e = -2;
+#define DTA_F1(HS_, N_, DV_) \
+  if (N_ == 1 && p.HS == HS_ && p.DV == DV_) { \
+    if constexpr (N_ == 1 && Plan<E, HS_, 1, DV_>::ok) e = launch_fwd_t<E, HS_, 1, DV_, DROP>(q, st); }
+  DTA_FOR_CONFIGS(DTA_F1)
+#undef DTA_F1
+  if (e) return e;
+  const int64_t n = (int64_t)p.B * p.T * p.H * (p.DV / (16 / (int)sizeof(E)));
+  hipLaunchKernelGGL((branch_combine_kernel<E, 0>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, p);
+  return (int)hipGetLastError();
+}
 
 template <class E, bool DROP>
 int dispatch_fwd(const FwdParams& p, hipStream_t st) {
 #define DTA_F(HS_, N_, DV_) \
   if (p.HS == HS_ && p.N == N_ && p.DV == DV_) { \
-    if constexpr (Plan<E, HS_, N_, DV_>::ok) return launch_fwd_t<E, HS_, N_, DV_, DROP>(p, st); else return -2; }
+    if constexpr (Plan<E, HS_, N_, DV_>::ok) return launch_fwd_t<E, HS_, N_, DV_, DROP>(p, st); }
   DTA_FOR_CONFIGS(DTA_F)
 #undef DTA_F
+  if (p.N >= 2) return fwd_branch_split_any<E, DROP>(p, st);
   return -2;
 }
 
+// the backward kernels take native branch counts only (capi.hip splits the others into groups)
 template <class E, bool DROP>
 int dispatch_dq(const BwdParams& p, hipStream_t st) {
 #define DTA_Q(HS_, N_, DV_) \
@@ -2181,14 +2229,6 @@ int dispatch_dkdv(const BwdParams& p, hipStream_t st) {
   DTA_FOR_CONFIGS(DTA_K)
 #undef DTA_K
   return -2;
-}
-
-template <class E>
-bool supported_t(int hs, int n, int dv) {
-#define DTA_S(HS_, N_, DV_) if (hs == HS_ && n == N_ && dv == DV_) return Plan<E, HS_, N_, DV_>::ok;
-  DTA_FOR_CONFIGS(DTA_S)
-#undef DTA_S
-  return false;
 }
 
 }  // namespace dta

@@ -23,9 +23,9 @@ int launch_attn_dq_f32_drop(const BwdParams&, hipStream_t);
 int launch_attn_dkdv_bf16_drop(const BwdParams&, hipStream_t);
 int launch_attn_dkdv_f16_drop(const BwdParams&, hipStream_t);
 int launch_attn_dkdv_f32_drop(const BwdParams&, hipStream_t);
-bool attn_supported_bf16(int, int, int);
-bool attn_supported_f16(int, int, int);
-bool attn_supported_f32(int, int, int);
+bool attn_native_bf16(int, int, int);
+bool attn_native_f16(int, int, int);
+bool attn_native_f32(int, int, int);
 
 int launch_attn_fwd(int dtype, const FwdParams& p, hipStream_t st) {
   if (p.drop_thr) switch (dtype) {
@@ -66,15 +66,28 @@ int launch_attn_dkdv(int dtype, const BwdParams& p, hipStream_t st) {
   }
   return -2;
 }
-bool attn_supported(int dtype, int hs, int n, int dv) {
+bool attn_native(int dtype, int hs, int n, int dv) {
   // dv = 2 hs (differential models) or, for standard attention (N = 1), dv = hs
   if (dv != 2 * hs && !(n == 1 && dv == hs)) return false;
   switch (dtype) {
-    case DTA_BF16: return attn_supported_bf16(hs, n, dv);
-    case DTA_F16: return attn_supported_f16(hs, n, dv);
-    case DTA_F32: return attn_supported_f32(hs, n, dv);
+    case DTA_BF16: return attn_native_bf16(hs, n, dv);
+    case DTA_F16: return attn_native_f16(hs, n, dv);
+    case DTA_F32: return attn_native_f32(hs, n, dv);
   }
   return false;
+}
+// Every branch count runs: natively, or -- where no N-branch plan is built (N >= 5, fp32
+// N = 3 / 4 at head sizes 96 / 128) -- as branch groups that each have one, on top of the
+// single-branch plan (the forward then runs branch-split, the backward group by group).
+bool attn_supported(int dtype, int hs, int n, int dv) {
+  if (n < 1) return false;
+  return attn_native(dtype, hs, n, dv) || (n >= 2 && dv == 2 * hs && attn_native(dtype, hs, 1, dv));
+}
+// size of the next branch group of the backward: the largest native branch count <= 4
+int branch_group(int dtype, int hs, int left, int dv) {
+  for (int g = left < 4 ? left : 4; g > 1; --g)
+    if (attn_native(dtype, hs, g, dv)) return g;
+  return 1;
 }
 }  // namespace dta
 
@@ -178,12 +191,13 @@ int dta_attn_fwd(const dta_attn_fwd_args* a, void* stream) {
   if (!attn_supported(a->dtype, a->head_size, a->n_terms, a->dv)) return DTA_ERR_UNSUPPORTED;
   if ((int64_t)a->B * a->T == 0) return DTA_OK;
   if (!ok_tensor(a->q, a->dtype, true) || !ok_tensor(a->k, a->dtype, true) || !ok_tensor(a->v, a->dtype, false) ||
-      !ok_tensor(a->o, a->dtype, false) || !ok_tensor(a->obr, a->dtype, true) || !a->lse || !a->coef)
+      !ok_tensor(a->o, a->dtype, false) || !ok_tensor(a->obr, DTA_F32, true) || !a->lse || !a->coef)
     return DTA_ERR_INVALID;
   p.q = t5(a->q); p.k = t5(a->k); p.v = t5(a->v); p.o = t5(a->o); p.obr = t5(a->obr);
   p.lse = a->lse; p.coef = a->coef;
   p.B = a->B; p.T = a->T; p.H = a->H; p.N = a->n_terms; p.HS = a->head_size; p.DV = a->dv;
   p.sl2 = a->scale * kLog2e;
+  p.cst = a->n_terms;
   p.stamps = stamp_buf();
   return status(launch_attn_fwd(a->dtype, p, (hipStream_t)stream));
 }
@@ -213,7 +227,7 @@ int dta_attn_bwd(const dta_attn_bwd_args* a, void* stream) {
   }
   if ((int64_t)a->B * a->T == 0) return DTA_OK;
   if (!ok_tensor(a->q, a->dtype, true) || !ok_tensor(a->k, a->dtype, true) || !ok_tensor(a->v, a->dtype, false) ||
-      !ok_tensor(a->obr, a->dtype, true) || !ok_tensor(a->dout, a->dtype, false) ||
+      !ok_tensor(a->obr, DTA_F32, true) || !ok_tensor(a->dout, a->dtype, false) ||
       !ok_tensor(a->dk, a->dtype, true) || !ok_tensor(a->dv_out, a->dtype, false) ||
       !a->lse || !a->coef || !a->delta)
     return DTA_ERR_INVALID;
@@ -228,13 +242,41 @@ int dta_attn_bwd(const dta_attn_bwd_args* a, void* stream) {
   p.dcoef_part = a->dcoef_partial;
   p.B = a->B; p.T = a->T; p.H = a->H; p.N = a->n_terms; p.HS = a->head_size; p.DV = a->dv;
   p.scale = a->scale; p.sl2 = a->scale * kLog2e;
+  p.cst = a->n_terms; p.br0 = 0; p.dv_acc = 0;
   p.stamps = stamp_buf();
+  // branch groups [g0, g0 + ng): a native N runs as one group; otherwise each group's
+  // branch-indexed operands are offset to its first branch (coef / dcoef rows keep the
+  // stride cst = N), so the kernels see an ng-branch problem
+  const int es = esize(a->dtype);
+  const int64_t rowvec = (int64_t)p.B * p.H * p.T, nblk = (p.T + 31) / 32;
+  auto group = [&](int g0, int ng) {
+    BwdParams q = p;
+    auto off = [&](T5& t) { t.p = (char*)t.p + (int64_t)g0 * t.si * es; };
+    off(q.q); off(q.k); off(q.dk);
+    q.obr.p = (char*)q.obr.p + (int64_t)g0 * q.obr.si * 4;        // fp32
+    if (q.dq.p) off(q.dq);
+    if (q.dq32) q.dq32 += (int64_t)g0 * p.HS;
+    q.lse += g0 * rowvec; q.delta += g0 * rowvec; q.coef += g0; q.dcoef += g0;
+    if (q.dcoef_part) q.dcoef_part += g0 * (int64_t)p.B * nblk;
+    q.N = ng; q.br0 = g0; q.dv_acc = g0 > 0;
+    return q;
+  };
   int e = 0;
-  if ((stages & DTA_BWD_DQ) && (e = launch_attn_dq(a->dtype, p, st))) return status(e);
-  if ((stages & DTA_BWD_DQ) && p.dcoef_part &&
-      (e = launch_dcoef_reduce(p.dcoef_part, p.dcoef, p.H, p.N, (int64_t)p.B * ((p.T + 31) / 32), st)))
-    return status(e);
-  if ((stages & DTA_BWD_DKDV) && (e = launch_attn_dkdv(a->dtype, p, st))) return status(e);
+  if (stages & DTA_BWD_DQ) {
+    for (int g0 = 0, ng; g0 < p.N; g0 += ng) {
+      ng = branch_group(a->dtype, p.HS, p.N - g0, p.DV);
+      if ((e = launch_attn_dq(a->dtype, group(g0, ng), st))) return status(e);
+    }
+    if (p.dcoef_part &&
+        (e = launch_dcoef_reduce(p.dcoef_part, p.dcoef, p.H, p.N, (int64_t)p.B * nblk, st)))
+      return status(e);
+  }
+  if (stages & DTA_BWD_DKDV) {
+    for (int g0 = 0, ng; g0 < p.N; g0 += ng) {
+      ng = branch_group(a->dtype, p.HS, p.N - g0, p.DV);
+      if ((e = launch_attn_dkdv(a->dtype, group(g0, ng), st))) return status(e);
+    }
+  }
   return DTA_OK;
 }
 

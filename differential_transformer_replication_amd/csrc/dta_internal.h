@@ -23,6 +23,7 @@ struct FwdParams {
   uint32_t drop_seed_lo, drop_seed_hi;
   int bsplit;          // launcher-internal: > 1 = branch-split launch of the N = 1 kernel
                        // (one branch of bsplit per workgroup; writes O_i and LSE_i only)
+  int cst;             // row stride of coef [h][cst] (the call's total branch count)
 };
 
 struct BwdParams {
@@ -40,6 +41,13 @@ struct BwdParams {
   uint32_t drop_thr;   // as FwdParams
   float drop_scale;
   uint32_t drop_seed_lo, drop_seed_hi;
+  // branch groups (capi: a call whose N has no kernel plan runs as groups of branches
+  // that have one; every branch-indexed pointer above is then offset to the group's
+  // first branch br0):
+  int cst;             // the call's total branch count: row stride of coef / dcoef
+                       // [h][cst], of the d(coef) partials and of dq32; dropout's branch index
+  int br0;             // the group's first branch (dropout mask key)
+  int dv_acc;          // dK/dV kernel: add into dv instead of storing (groups after the first)
 };
 
 // per-dtype launchers (dtype index: 0 bf16, 1 f16, 2 f32); return hipError_t
@@ -50,7 +58,8 @@ int launch_attn_dq_drop(int dtype, const BwdParams& p, hipStream_t st);
 int launch_attn_dkdv_drop(int dtype, const BwdParams& p, hipStream_t st);
 int launch_attn_dq(int dtype, const BwdParams& p, hipStream_t st);
 int launch_attn_dkdv(int dtype, const BwdParams& p, hipStream_t st);
-bool attn_supported(int dtype, int hs, int n, int dv);
+bool attn_supported(int dtype, int hs, int n, int dv);   // any kernel path: native plan or branch groups
+bool attn_native(int dtype, int hs, int n, int dv);      // an N-branch kernel plan is built
 
 struct LnParams {
   int64_t rows, C;
@@ -80,12 +89,6 @@ struct RopeParams {
   int inverse;
 };
 
-struct DeltaParams {
-  T5 dout, obr;
-  float* delta;
-  int B, T, H, N, DV;
-};
-
 #ifndef DTA_DECODE_CHUNK
 #define DTA_DECODE_CHUNK 256   // keys per workgroup of the split-key decode plan
 #endif
@@ -103,8 +106,6 @@ struct DecodeParams {
 int launch_decode(int dtype, const DecodeParams& p, hipStream_t st);
 int launch_ln(int dtype, const LnParams& p, bool bwd, hipStream_t st);
 int launch_rope(int dtype, bool src_f32, const RopeParams& p, hipStream_t st);
-int launch_delta(int dtype, const DeltaParams& p, hipStream_t st);
-int launch_dcoef(const float* delta, float* dcoef, int B, int T, int H, int N, hipStream_t st);
 int launch_dcoef_reduce(const float* part, float* dcoef, int H, int N, int64_t per, hipStream_t st);
 int launch_cast(int dtype, const float* src, const T5& dst, int B, int T, int H, int N, int HS, hipStream_t st);
 

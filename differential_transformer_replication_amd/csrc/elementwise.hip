@@ -449,50 +449,6 @@ __global__ __launch_bounds__(256) void rope_kernel(RopeParams p) {
 }
 
 
-// one group of G = DV/8 lanes per (b, t, h) row; each lane one 16-byte vector
-template <class E>
-__global__ __launch_bounds__(256) void bwd_delta_kernel(DeltaParams p) {
-  const int G = p.DV / 8;                       // lanes per row (<= 64)
-  const int lane = threadIdx.x & 63;
-  const int rows_per_wave = 64 / G;
-  const int64_t nrows = (int64_t)p.B * p.T * p.H;
-  const int64_t wave_id = ((int64_t)blockIdx.x * 256 + threadIdx.x) / 64;
-  const int64_t row = wave_id * rows_per_wave + lane / G;
-  const int sub = lane % G;
-  const bool ok = row < nrows;
-  const int h = ok ? (int)(row % p.H) : 0;
-  const int t = ok ? (int)((row / p.H) % p.T) : 0;
-  const int b = ok ? (int)(row / ((int64_t)p.H * p.T)) : 0;
-  float dov[8];
-  if (ok) ld8<E>(reinterpret_cast<const E*>(p.dout.p) + b * p.dout.sb + (int64_t)t * p.dout.st + h * p.dout.sh + sub * 8, dov);
-  for (int i = 0; i < p.N; ++i) {
-    float s = 0.f;
-    if (ok) {
-      float ov[8];
-      ld8<E>(reinterpret_cast<const E*>(p.obr.p) + i * p.obr.si + b * p.obr.sb + (int64_t)t * p.obr.st + h * p.obr.sh + sub * 8, ov);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) s = fmaf(dov[j], ov[j], s);
-    }
-    for (int o = G / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-    if (ok && sub == 0) p.delta[(((int64_t)i * p.B + b) * p.H + h) * p.T + t] = s;
-  }
-}
-
-// dcoef[h][i] = sum over b, t of delta[i][b][h][t]; one block per (h, i)
-__global__ __launch_bounds__(256) void dcoef_kernel(const float* delta, float* dcoef, int B, int T, int H, int N) {
-  const int h = blockIdx.x / N, i = blockIdx.x % N;
-  float s = 0.f;
-  for (int b = 0; b < B; ++b) {
-    const float* d = delta + (((int64_t)i * B + b) * H + h) * T;
-    for (int t = threadIdx.x; t < T; t += 256) s += d[t];
-  }
-  s = wave_sum(s);
-  __shared__ float part[4];
-  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
-  __syncthreads();
-  if (threadIdx.x == 0) dcoef[h * N + i] = part[0] + part[1] + part[2] + part[3];
-}
-
 template <class E>
 __global__ __launch_bounds__(256) void cast_f32_kernel(const float* src, T5 dst, int B, int T, int H, int N, int HS) {
   const int per_row = HS / 8;
@@ -610,26 +566,6 @@ int launch_rope(int dtype, bool src_f32, const RopeParams& p, hipStream_t st) {
     default: return -2;
   }
 #undef DTA_R
-  return (int)hipGetLastError();
-}
-
-int launch_delta(int dtype, const DeltaParams& p, hipStream_t st) {
-  const int64_t nrows = (int64_t)p.B * p.T * p.H;
-  if (nrows == 0) return 0;
-  const int rows_per_wave = 64 / (p.DV / 8);
-  const int64_t waves = (nrows + rows_per_wave - 1) / rows_per_wave;
-  dim3 g((unsigned)((waves + 3) / 4));
-  switch (dtype) {
-    case 0: hipLaunchKernelGGL(bwd_delta_kernel<__bf16>, g, dim3(256), 0, st, p); break;
-    case 1: hipLaunchKernelGGL(bwd_delta_kernel<_Float16>, g, dim3(256), 0, st, p); break;
-    case 2: hipLaunchKernelGGL(bwd_delta_kernel<float>, g, dim3(256), 0, st, p); break;
-    default: return -2;
-  }
-  return (int)hipGetLastError();
-}
-
-int launch_dcoef(const float* delta, float* dcoef, int B, int T, int H, int N, hipStream_t st) {
-  hipLaunchKernelGGL(dcoef_kernel, dim3(H * N), dim3(256), 0, st, delta, dcoef, B, T, H, N);
   return (int)hipGetLastError();
 }
 

@@ -39,9 +39,12 @@ __all__ = ["KVCache", "DecodeGraph", "DevicePosition", "cached_generate", "enabl
 def enabled(idx: torch.Tensor, model=None) -> bool:
     if not idx.is_cuda or os.environ.get("DTA_KV_CACHE", "1") == "0":
         return False
-    if model is not None:      # a fused plan must exist for the prefill (control: hs 64 / 128)
+    if model is not None:
+        # the prefill runs on the fused kernels (ops.diff_attention: any built or padded head
+        # size, any branch count); the decode kernel takes head sizes % 8 up to 128, N <= 4
         _, _, N, hs, dv, _ = _spec(model.blocks[0])
-        return ops.supported(model.lm_head.weight.dtype, hs, N, dv)
+        return (ops.attention_supported(model.lm_head.weight.dtype, hs, N, dv) and N <= 4 and hs % 8 == 0
+                and hs <= 128)
     return True
 
 

@@ -72,8 +72,28 @@ TIMER = KernelTimer()
 
 
 def supported(dtype: torch.dtype, hs: int, N: int, dv: int) -> bool:
-    """Whether libdiffattn.so has a gfx950 kernel plan for this shape (dta_supported)."""
+    """Whether libdiffattn.so runs this shape as it is (dta_supported): an N-branch
+    kernel plan, or branch groups over such plans for branch counts without one."""
     return bool(_lib.load().dta_supported(_lib.dtype_code(dtype), hs, N, dv))
+
+
+def padded_head(dtype: torch.dtype, hs: int, N: int, dv: int) -> Optional[int]:
+    """The head size the kernels run a head of size ``hs`` at: ``hs`` itself when it is
+    built, else the smallest built head size above it (Q_i / K_i and V zero-padded, see
+    ``diff_attention``), else None.  The reference accepts any head size
+    (head_size = n_embd // (2 n_head), diff_transformer.py:111); the plans are built for
+    16, 32, 64, 96 and 128."""
+    if N < 1 or hs < 1 or dv not in (hs, 2 * hs) or (dv == hs and N != 1):
+        return None
+    for hp in (hs,) + tuple(h for h in (16, 32, 64, 96, 128) if h > hs):
+        if supported(dtype, hp, N, hp if dv == hs else 2 * hp):
+            return hp
+    return None
+
+
+def attention_supported(dtype: torch.dtype, hs: int, N: int, dv: int) -> bool:
+    """Whether ``diff_attention`` runs this shape on the HIP kernels (directly or padded)."""
+    return padded_head(dtype, hs, N, dv) is not None
 
 
 def packed_width(H: int, N: int, hs: int, dv: int) -> int:
@@ -93,7 +113,7 @@ def split_packed(qkv: Tensor, H: int, N: int, hs: int, dv: int):
 class _DiffAttention(torch.autograd.Function):
     @staticmethod
     def forward(ctx, qkv: Tensor, coef: Tensor, H: int, N: int, hs: int, freqs: Optional[Tensor], dv: int,
-                dropout_p: float, seed: int):
+                dropout_p: float, seed: int, scale: float):
         lib = _lib.load()
         _require_gpu(qkv, coef)
         if qkv.dim() != 3:
@@ -119,16 +139,16 @@ class _DiffAttention(torch.autograd.Function):
             _lib.check(lib.dta_rope(ra, stream))
             q, k = qk_rot[:, :, :H], qk_rot[:, :, H:]
         o = torch.empty(B, T, H, dv, device=dev, dtype=qkv.dtype)
-        obr = torch.empty(N, B, T, H, dv, device=dev, dtype=qkv.dtype)
+        obr = torch.empty(N, B, T, H, dv, device=dev, dtype=torch.float32)   # fp32 O_i (delta_i, d(coef))
         lse = torch.empty(N, B, H, T, device=dev, dtype=torch.float32)
         obr_t = _lib.DtaTensor(obr.data_ptr(), *obr.stride()[1:4], obr.stride(0))
-        a = _lib.AttnFwdArgs(dt, B, T, H, N, hs, dv, 1.0 / math.sqrt(hs), dropout_p,
+        a = _lib.AttnFwdArgs(dt, B, T, H, N, hs, dv, scale, dropout_p,
                              _lib.tensor5(q), _lib.tensor5(k), _lib.tensor5(v), _lib.tensor5(o), obr_t,
                              lse.data_ptr(), coef.data_ptr(), seed)
         with TIMER.region("attn_fwd"):
             _lib.check(lib.dta_attn_fwd(a, stream))
         ctx.save_for_backward(qkv, qk_rot, obr, lse, coef, freqs)
-        ctx.dims = (H, N, hs, dv)
+        ctx.dims = (H, N, hs, dv, scale)
         ctx.drop = (dropout_p, seed)
         return o.view(B, T, H * dv)
 
@@ -136,7 +156,7 @@ class _DiffAttention(torch.autograd.Function):
     def backward(ctx, do: Tensor):
         lib = _lib.load()
         qkv, qk_rot, obr, lse, coef, freqs = ctx.saved_tensors
-        H, N, hs, dv = ctx.dims
+        H, N, hs, dv, scale = ctx.dims
         B, T, W = qkv.shape
         dev = qkv.device
         stream = _lib.stream_handle(dev)
@@ -154,7 +174,7 @@ class _DiffAttention(torch.autograd.Function):
         # with RoPE the kernels differentiate w.r.t. the rotated Q/K (qk_rot) and their
         # dQ / dK epilogues apply the inverse rotation, writing straight into dqkv
         obr_t = _lib.DtaTensor(obr.data_ptr(), *obr.stride()[1:4], obr.stride(0))
-        a = _lib.AttnBwdArgs(dt, B, T, H, N, hs, dv, 1.0 / math.sqrt(hs), ctx.drop[0],
+        a = _lib.AttnBwdArgs(dt, B, T, H, N, hs, dv, scale, ctx.drop[0],
                              _lib.tensor5(q), _lib.tensor5(k), _lib.tensor5(v), obr_t,
                              lse.data_ptr(), coef.data_ptr(), _lib.tensor5(do),
                              _lib.tensor5(dq), _lib.tensor5(dk), _lib.tensor5(dvv),
@@ -167,7 +187,7 @@ class _DiffAttention(torch.autograd.Function):
         a.stages = _lib.BWD_DKDV
         with TIMER.region("attn_bwd_dkdv"):
             _lib.check(lib.dta_attn_bwd(a, stream))
-        return dqkv, dcoef, None, None, None, None, None, None, None
+        return dqkv, dcoef, None, None, None, None, None, None, None, None
 
 
 def diff_attention(qkv: Tensor, coef: Tensor, H: int, N: int, hs: int,
@@ -190,7 +210,30 @@ def diff_attention(qkv: Tensor, coef: Tensor, H: int, N: int, hs: int,
         raise ValueError(f"dropout probability has to be in [0, 1), got {dropout_p}")
     if seed is None:
         seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if dropout_p > 0 else 0
-    return _DiffAttention.apply(qkv, coef, H, N, hs, freqs, 2 * hs if dv is None else dv, dropout_p, int(seed))
+    dv = 2 * hs if dv is None else dv
+    scale = 1.0 / math.sqrt(hs)                 # diff_transformer.py:57, of the true head size
+    hp = padded_head(qkv.dtype, hs, N, dv) if qkv.is_cuda else hs
+    if hp is None:
+        raise RuntimeError(f"no gfx950 kernel for head_size={hs}, n_terms={N}, dv={dv}, dtype={qkv.dtype} "
+                           "(head sizes up to 128 are served)")
+    if hp == hs:
+        return _DiffAttention.apply(qkv, coef, H, N, hs, freqs, dv, dropout_p, int(seed), scale)
+    # a head size without its own plan runs in the next built one: Q_i / K_i zero-padded
+    # to hp columns leave every score Q_i K_i^T unchanged (the softmax scale stays
+    # 1/sqrt(hs)), V padded to dvp columns adds zero output columns, which are dropped;
+    # the pad columns' gradients are discarded by the slices' backward
+    dvp = hp if dv == hs else 2 * hp
+    B, T, _ = qkv.shape
+    q, k, v = split_packed(qkv, H, N, hs, dv)
+    qkv_p = torch.cat([F.pad(q, (0, hp - hs)).flatten(2), F.pad(k, (0, hp - hs)).flatten(2),
+                       F.pad(v, (0, dvp - dv)).flatten(2)], dim=-1)
+    if freqs is not None:
+        # identity rotation (cos 1, sin 0) on the pad pairs: they stay zero
+        pad = torch.zeros(freqs.shape[0], (hp - hs) // 2, 2, device=freqs.device, dtype=freqs.dtype)
+        pad[..., 0] = 1.0
+        freqs = torch.cat([freqs, pad], dim=1).contiguous()
+    out = _DiffAttention.apply(qkv_p, coef, H, N, hp, freqs, dvp, dropout_p, int(seed), scale)
+    return out.view(B, T, H, dvp)[..., :dv].reshape(B, T, H * dv)
 
 
 class _GroupLNScale(torch.autograd.Function):

@@ -17,7 +17,7 @@
  *  - Every launch is asynchronous on the given stream; no host sync.
  *  - Functions return DTA_OK (0) or a negative error code and never throw
  *    across the ABI; dta_error_string() describes a code.
- *  - dtype applies to Q/K/V/O/dO/dQ/dK/dV activations; LSE, delta, the
+ *  - dtype applies to Q/K/V/O/dO/dQ/dK/dV activations; Obr, LSE, delta, the
  *    coefficients, the LayerNorm statistics/parameters and every *_f32 buffer
  *    are always fp32.
  *
@@ -26,7 +26,8 @@
  *   Q, K   [b][t][h][i][d]   i < n_terms (the N softmax branches), d < head_size
  *   V, O   [b][t][h][e]      e < dv (dv = 2*head_size for diff attention; dv = head_size with n_terms = 1
  *                             for standard attention, head_size 64 or 128)
- *   Obr    [i][b][t][h][e]   per-branch normalised outputs A_i V (saved for bwd)
+ *   Obr    [i][b][t][h][e]   fp32 per-branch normalised outputs A_i V (saved for bwd:
+ *                             delta_i = <dO, O_i> and d(coef) come from them)
  *   LSE    [i][b][h][t]      fp32, NEGATED log2-sum-exp of the scaled scores (-log2 sum 2^(s*scale*log2e))
  *   coef   [h][i]            fp32, signed branch weights (diff: [1, -lambda];
  *                            N-diff: [+l0, -l1, +l2, ...])
@@ -41,7 +42,7 @@
 extern "C" {
 #endif
 
-#define DTA_ABI_VERSION 3
+#define DTA_ABI_VERSION 4   /* 4: Obr is fp32 for every dtype; any n_terms >= 1 */
 
 enum dta_dtype { DTA_BF16 = 0, DTA_F16 = 1, DTA_F32 = 2 };
 
@@ -257,7 +258,13 @@ int dta_cast_f32(int32_t dtype, int32_t B, int32_t T, int32_t H, int32_t n_terms
 
 const char* dta_error_string(int code);
 int dta_abi_version(void);
-/* 1 if (dtype, head_size, n_terms, dv) has compiled kernels. */
+/* 1 if (dtype, head_size, n_terms, dv) runs: an n_terms-branch kernel plan is built for
+ * it, or (n_terms >= 2, dv = 2*head_size) the single-branch plan is -- then the forward
+ * runs n_terms single-branch workgroups per query block and head plus a combine pass,
+ * and the backward runs branch groups of the largest built branch count (<= 4) one after
+ * another (dV summed over the groups, d(coef) reduced over all n_terms).  Head sizes
+ * 16, 32, 64, 96, 128 (dv = 2*head_size), and dv = head_size at n_terms = 1 for 32, 64,
+ * 96, 128; the Python layer runs other head sizes up to 128 zero-padded to the next one. */
 int dta_supported(int32_t dtype, int32_t head_size, int32_t n_terms, int32_t dv);
 
 #ifdef __cplusplus

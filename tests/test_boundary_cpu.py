@@ -37,7 +37,27 @@ def test_library_loads_and_exports():
     assert _lib.supported(torch.bfloat16, 64, 2, 128)
     assert _lib.supported(torch.float32, 16, 4, 32)
     assert not _lib.supported(torch.bfloat16, 64, 2, 96)     # dv must be 2*hs
-    assert not _lib.supported(torch.bfloat16, 48, 2, 96)     # head size not built
+    assert not _lib.supported(torch.bfloat16, 48, 2, 96)     # head size not built (the Python layer pads it)
+    # branch counts without an N-branch plan run as branch groups (csrc/capi.hip)
+    for dt in (torch.bfloat16, torch.float16, torch.float32):
+        for hs in (16, 32, 64, 96, 128):
+            for n in range(1, 9):
+                assert _lib.supported(dt, hs, n, 2 * hs), (dt, hs, n)
+    assert not _lib.supported(torch.bfloat16, 64, 0, 128)
+
+
+def test_padded_head_sizes_without_gpu():
+    """ops.padded_head: head sizes without a plan run in the next built one (diff: dv = 2 hs;
+    control: N = 1, dv = hs), up to 128."""
+    from differential_transformer_replication_amd import ops
+    assert ops.padded_head(torch.bfloat16, 64, 2, 128) == 64
+    assert ops.padded_head(torch.bfloat16, 48, 2, 96) == 64
+    assert ops.padded_head(torch.float32, 8, 5, 16) == 16
+    assert ops.padded_head(torch.bfloat16, 100, 3, 200) == 128
+    assert ops.padded_head(torch.bfloat16, 80, 1, 80) == 96
+    assert ops.padded_head(torch.bfloat16, 16, 1, 16) == 32
+    assert ops.padded_head(torch.bfloat16, 136, 2, 272) is None
+    assert ops.padded_head(torch.bfloat16, 64, 2, 64) is None        # dv = hs only for N = 1
 
 
 def test_invalid_args_rejected_without_gpu():

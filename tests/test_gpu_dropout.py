@@ -78,6 +78,9 @@ DROP_CASES = [  # H, N, hs, T, dv, rope, p
     (1, 2, 64, 700, 128, False, 0.2),
     # branch-split forward (one branch per workgroup + combine) with the mask: N = 3 / 4 at hs = 64
     (2, 3, 64, 150, 128, True, 0.2), (1, 4, 64, 100, 128, False, 0.1),
+    # branch counts without an N-branch plan (branch-split forward, grouped backward: the
+    # mask keys keep the call's branch index and count), a zero-padded head size
+    (1, 5, 64, 130, 128, True, 0.2), (1, 6, 32, 100, 64, False, 0.1), (1, 2, 48, 90, 96, False, 0.2),
 ]
 
 
@@ -86,8 +89,7 @@ DROP_CASES = [  # H, N, hs, T, dv, rope, p
 def test_dropout_matches_restated_masks(dtype, H, N, hs, T, dv, rope, p):
     ops = _ops()
     from differential_transformer_replication_amd import _lib
-    if not _lib.supported(dtype, hs, N, dv):
-        pytest.skip("configuration not built")
+    assert ops.attention_supported(dtype, hs, N, dv)
     g = torch.Generator().manual_seed(7 * T + N)
     B, seed = 2, 0x1234_5678_9ABC + T
     W = ops.packed_width(H, N, hs, dv)

@@ -63,7 +63,7 @@ def main():
 
     def bufs():
         o = torch.empty(B, T, H, dv, device=dev, dtype=torch.bfloat16)
-        obr = torch.empty(N, B, T, H, dv, device=dev, dtype=torch.bfloat16)
+        obr = torch.empty(N, B, T, H, dv, device=dev, dtype=torch.float32)
         lse = torch.empty(N, B, H, T, device=dev)
         dqkv = torch.zeros_like(qkv)
         dcoef = torch.empty(H, N, device=dev)

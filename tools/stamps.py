@@ -48,7 +48,7 @@ def main():
     k = qkv[..., nq:2 * nq].unflatten(-1, (H, N, hs))
     v = qkv[..., 2 * nq:].unflatten(-1, (H, dv))
     o = torch.empty(B, T, H, dv, device=dev, dtype=torch.bfloat16)
-    obr = torch.empty(N, B, T, H, dv, device=dev, dtype=torch.bfloat16)
+    obr = torch.empty(N, B, T, H, dv, device=dev, dtype=torch.float32)
     lse = torch.empty(N, B, H, T, device=dev)
     dqkv = torch.zeros_like(qkv)
     dcoef = torch.empty(H, N, device=dev)
