@@ -1466,6 +1466,395 @@ void attn_dq_kernel(BwdParams p) {
       }
 }
 
+// ------------------------------------- backward: dQ, two query blocks per wave ---
+// attn_dq2_kernel: the query-major backward of attn_dq_kernel re-planned for one wave per
+// SIMD.  A wave owns TWO 32-row query blocks (64 rows; the workgroup's 4 waves 256 rows)
+// and the whole 512-entry register file: the dQ accumulators of both blocks, their dO
+// rows, the dP and S' accumulators and the packed dS of every (branch, block) unit of a
+// tile.  Q_i (all branches, prescaled by sl2) sit in LDS; K_i / V tiles of 64 keys stream
+// through the LDS-DMA ring as in attn_dq_kernel.
+//
+// Per tile the work is two streams: MFMAs (per unit u = (branch, block): the seeded S'
+// chain; per block the seeded dP chain; per unit the dQ product) and VALU (per unit:
+// exp2, the dS multiply, the bf16 pack).  With no partner wave on the SIMD, the VALU of a
+// unit has to run in the gaps of MFMAs that do not depend on it.  Dq2Sched lays the tile
+// out at compile time: a fixed MFMA order (S'(u0) dP(0) S'(u1) dP(1) S'(u2) dQ(u0) S'(u3)
+// dQ(u1) ... dQ(u_last)), every LDS operand read issued R MFMAs ahead of its consumer
+// (inline asm, counted lgkmcnt), and each unit's VALU split into 16 pieces (two elements
+// each) placed earliest-deadline-first into the MFMA slots between the end of its inputs
+// and the first MFMA that needs its result or its registers.  A sched_barrier closes
+// every slot, so the compiler keeps the placement.
+#ifndef DTA_DQ2
+#define DTA_DQ2 1
+#endif
+#ifndef DTA_DQ2_R
+#define DTA_DQ2_R 2          // MFMAs of read-ahead
+#endif
+// bf16 MFMA accumulating into AGPRs (inline asm): the dQ accumulators are touched only by
+// MFMAs, so they live in the AGPR half of the register file while everything the VALU
+// reads stays in VGPRs (the unit is built with -mllvm -amdgpu-mfma-vgpr-form=1, which
+// selects VGPR accumulators for the builtins).  The hazard recognizer does not see inside
+// the asm: NOP = 1 adds the two wait states a VALU-written operand needs, and the caller
+// waits before reading the accumulators (dq2_acc_fence).
+template <bool NOP>
+__device__ __forceinline__ void mfma_agpr(f32x16& acc, bf16x8 a, bf16x8 b) {
+  if constexpr (NOP) asm("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+  else asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+__device__ __forceinline__ void dq2_acc_fence() { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory"); }
+
+namespace dq2 {
+enum : int { SS = 0, SC = 1, DS = 2, DC = 3, CC = 4 };
+struct Op { int kind = 0, u = 0, qb = 0, i = 0, a = 0, b = 0, c = 0; };
+constexpr int PIECES = 16;     // VALU pieces per unit: 2 key blocks x 16 elements, two at a time
+
+template <int N, int NSQ, int NSV, int NHB>
+struct Sched {
+  static constexpr int NKB = 2, U = 2 * N, SR = 2;            // S' accumulator sets in flight
+  static constexpr int NS1 = NKB + NSQ * NKB, ND1 = NKB + NSV * NKB, NC1 = NHB * NKB * 2;
+  static constexpr int NOPS = U * NS1 + 2 * ND1 + U * NC1;
+  // unit u -> branch (highest first: branch 0's VALU, without the delta add, is the lightest) and block
+  static constexpr int ui(int u) { return N - 1 - u / 2; }
+  static constexpr int uq(int u) { return u % 2; }
+  Op ops[NOPS];
+  int s0[U] = {}, s1[U] = {}, c0[U] = {}, d1[2] = {};
+  int E[U] = {}, Dl[U] = {};
+  int pslot[U][PIECES] = {};
+  int npiece[NOPS] = {};       // VALU pieces in slot s
+  int pu[NOPS][PIECES] = {};   // ... which (unit, piece): u * PIECES + j
+  int nreads[NOPS] = {};       // LDS read instructions op s issues (at slot s - R)
+  int rid[NOPS] = {};          // index of op s's b128 read among all b128 reads (K / V / Q frags)
+  int qid[NOPS] = {};          // Q fragment read index (S' ops with b == 0)
+  int tid[NOPS] = {};          // tr block index (dQ ops with c == 0)
+  bool ok = true;
+  constexpr void add_s(int& n, int u) {
+    s0[u] = n;
+    for (int kb = 0; kb < NKB; ++kb) { ops[n].kind = SS; ops[n].u = u; ops[n].qb = uq(u); ops[n].i = ui(u); ops[n].b = kb; ++n; }
+    for (int st = 0; st < NSQ; ++st)
+      for (int kb = 0; kb < NKB; ++kb) {
+        ops[n].kind = SC; ops[n].u = u; ops[n].qb = uq(u); ops[n].i = ui(u); ops[n].a = st; ops[n].b = kb; ++n;
+      }
+    s1[u] = n - 1;
+  }
+  constexpr void add_d(int& n, int qb) {
+    for (int kb = 0; kb < NKB; ++kb) { ops[n].kind = DS; ops[n].qb = qb; ops[n].b = kb; ++n; }
+    for (int s = 0; s < NSV; ++s)
+      for (int kb = 0; kb < NKB; ++kb) { ops[n].kind = DC; ops[n].qb = qb; ops[n].a = s; ops[n].b = kb; ++n; }
+    d1[qb] = n - 1;
+  }
+  constexpr void add_c(int& n, int u) {
+    c0[u] = n;
+    for (int d = 0; d < NHB; ++d)
+      for (int kb = 0; kb < NKB; ++kb)
+        for (int ks = 0; ks < 2; ++ks) {
+          ops[n].kind = CC; ops[n].u = u; ops[n].qb = uq(u); ops[n].i = ui(u); ops[n].a = d; ops[n].b = kb; ops[n].c = ks; ++n;
+        }
+  }
+  constexpr Sched() {
+    int n = 0;
+    add_s(n, 0); add_d(n, 0);
+    if (U > 1) { add_s(n, 1); add_d(n, 1); }
+    for (int u = 2; u < U; ++u) { add_s(n, u); add_c(n, u - 2); }
+    for (int u = (U > 2 ? U - 2 : 0); u < U; ++u) add_c(n, u);
+    if (n != NOPS) ok = false;
+    // VALU windows: after the unit's S' and dP chains, before its dQ product and before the
+    // S' chain that reuses its accumulator set
+    for (int u = 0; u < U; ++u) {
+      E[u] = (s1[u] > d1[uq(u)] ? s1[u] : d1[uq(u)]) + 1;
+      Dl[u] = c0[u] - 1;       // the last pack at least one MFMA before its dQ product
+      if (u + SR < U && s0[u + SR] < Dl[u]) Dl[u] = s0[u + SR];
+    }
+    // each unit's pieces in order over its window, up to the lowest per-slot cap that fits
+    int load[NOPS] = {};
+    for (int u = 0; u < U; ++u) {
+      int cap = 1;
+      for (;; ++cap) {
+        int room = 0;
+        for (int x = E[u]; x < Dl[u]; ++x) room += load[x] < cap ? cap - load[x] : 0;
+        if (room >= PIECES || cap >= PIECES) break;
+      }
+      int j = 0;
+      for (int x = E[u]; x < Dl[u] && j < PIECES; ++x)
+        while (load[x] < cap && j < PIECES) {
+          pslot[u][j] = x;
+          if (npiece[x] < PIECES) pu[x][npiece[x]++] = u * PIECES + j; else ok = false;
+          ++load[x];
+          ++j;
+        }
+      if (j < PIECES) ok = false;
+    }
+    int nb = 0, nq = 0, ntr = 0;
+    for (int s = 0; s < NOPS; ++s) {
+      const Op& o = ops[s];
+      if (o.kind == SC) {
+        rid[s] = nb++; nreads[s] = 1;
+        if (o.b == 0) { qid[s] = nq++; nreads[s] = 2; }
+      } else if (o.kind == DC) {
+        rid[s] = nb++; nreads[s] = 1;
+      } else if (o.kind == CC && o.c == 0) {
+        tid[s] = ntr++; nreads[s] = 4;
+      }
+    }
+  }
+  // LDS read instructions issued for ops (s, s + R]: lgkmcnt at op s
+  constexpr int pending(int s, int R) const {
+    int c = 0;
+    for (int x = s + 1; x <= s + R && x < NOPS; ++x) c += nreads[x];
+    return c;
+  }
+};
+template <int N, int NSQ, int NSV, int NHB>
+struct Hold { static constexpr Sched<N, NSQ, NSV, NHB> v{}; };
+}  // namespace dq2
+
+template <class E, int HS, int N, int DV>
+struct Dq2Cfg {
+  static constexpr int NW = 4, BM = 256, BN = 64;
+  static constexpr int nQ = N * BM * HS, nK = N * BN * HS, nV = BN * DV;
+  static constexpr int NS = ring_stages(nQ * (int)sizeof(E), (nK + nV) * (int)sizeof(E));
+  static constexpr int bytes = (nQ + NS * (nK + nV)) * (int)sizeof(E);
+  static constexpr int NHB = HS / 32;
+  // per-lane registers: dQ accumulators, dO rows, dP, two S' sets, packed dS of every
+  // unit, seeds, read buffers and addresses
+  static constexpr int regs = 2 * N * NHB * 16 + 2 * DV / 4 + 2 * 2 * 16 + 2 * 2 * 16 + 2 * N * 16 + 8 * N + 92;
+  static constexpr bool shape_ok = DTA_DQ2 && std::is_same<E, __bf16>::value && (HS == 32 || HS == 64 || HS == 128) &&
+                                   (DV == HS || DV == 2 * HS) && DV <= 128 && bytes <= 160 * 1024 && regs <= 512;
+  template <bool S, int = 0> struct Sok { static constexpr bool v = false; };
+  template <int X> struct Sok<true, X> { static constexpr bool v = dq2::Hold<N, HS / 16, DV / 16, HS / 32>::v.ok; };
+  static constexpr bool ok = Sok<shape_ok>::v;
+};
+
+template <class E, int HS, int N, int DV>
+__global__ __launch_bounds__(256, 1)
+void attn_dq2_kernel(BwdParams p) {
+  using O = Ops<E>;
+  using frag = typename O::frag;
+  using CF = Dq2Cfg<E, HS, N, DV>;
+  constexpr int NW = CF::NW, BM = CF::BM, BN = CF::BN, NTHR = NW * 64, KS = O::KSTEP;
+  constexpr int NSQ = HS / KS, NSV = DV / KS, NHB = HS / 32, NKB = 2, NS = CF::NS;
+  constexpr int ROWB = HS * (int)sizeof(E), VROWB = DV * (int)sizeof(E);
+  constexpr int R = DTA_DQ2_R;
+  using SCH = dq2::Hold<N, NSQ, NSV, NHB>;
+  constexpr int NOPS = dq2::Sched<N, NSQ, NSV, NHB>::NOPS;
+  constexpr int U = 2 * N;
+  static_assert(SCH::v.ok, "dQ2 schedule");
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  E* Qs = reinterpret_cast<E*>(smem);   // [N][BM][HS], prescaled by sl2
+  E* Kb = Qs + CF::nQ;                  // [NS][N][BN][HS]
+  E* Vb = Kb + NS * CF::nK;             // [NS][BN][DV]
+
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int tid = threadIdx.x, lane = tid & 63;
+  int hf = lane >> 5, c32 = lane & 31;
+  int bx, by, bz, lin;
+  lpt_order(bx, by, bz, lin);
+  const int qt = gridDim.x - 1 - bx;
+  const int hh = by, b = bz;
+  const int T = p.T;
+  const int q0 = qt * BM, qw0 = q0 + wave * 64;
+
+  const E* gq = reinterpret_cast<const E*>(p.q.p) + b * p.q.sb + hh * p.q.sh;
+  const E* gk = reinterpret_cast<const E*>(p.k.p) + b * p.k.sb + hh * p.k.sh;
+  const E* gv = reinterpret_cast<const E*>(p.v.p) + b * p.v.sb + hh * p.v.sh;
+  const E* gdo = reinterpret_cast<const E*>(p.dout.p) + b * p.dout.sb + hh * p.dout.sh;
+  const float* gob = reinterpret_cast<const float*>(p.obr.p) + b * p.obr.sb + hh * p.obr.sh;
+  const int kend = min(T, q0 + BM);
+  const int ntiles = (kend + BN - 1) / BN;
+  using KR = KvRing<E, HS, N, DV, BN, NW>;
+  uint32_t doff[KR::MYP];
+  KR::offsets(p.k.st, p.k.si, p.v.st, wave, lane, doff);
+  auto stage_kv = [&](int kt, int buf) {
+    KR::issue_pre(gk, p.k.st, gv, p.v.st, kt * BN, T, Kb + buf * CF::nK, Vb + buf * CF::nV, wave, doff);
+  };
+
+  // ---- per-block row operands: dO rows (B operands of dP), delta, LSE seeds
+  frag df[2][NSV];
+  frag f_one = O::zero(), f_lse[2][N], f_dp[2];
+  float coef[N], dd[2][N];
+  const int64_t bstride = (int64_t)p.B * p.H * T;
+#pragma unroll
+  for (int i = 0; i < N; ++i) coef[i] = p.coef[hh * p.cst + i];
+  if (hf == 0) { f_one[0] = (E)1.f; f_one[1] = (E)1.f; }
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const int qrow = qw0 + 32 * qb + c32;
+    const bool rowok = qrow < T;
+    const int64_t rs = ((int64_t)b * p.H + hh) * T + qrow;
+#pragma unroll
+    for (int s = 0; s < NSV; ++s)
+      df[qb][s] = rowok ? O::load_global(gdo + (int64_t)qrow * p.dout.st + s * KS + hf * O::KH) : O::zero();
+    float del0 = 0.f;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const float lse = rowok ? p.lse[rs + i * bstride] : 0.f;
+      float d = 0.f;
+      if (rowok) {
+#pragma unroll
+        for (int s = 0; s < NSV; ++s) {
+          const float* o = gob + (int64_t)qrow * p.obr.st + i * p.obr.si + s * KS + hf * O::KH;
+          const f32x4 o0 = *reinterpret_cast<const f32x4*>(o), o1 = *reinterpret_cast<const f32x4*>(o + 4);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) d = fmaf((float)df[qb][s][j], o0[j], d);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) d = fmaf((float)df[qb][s][4 + j], o1[j], d);
+        }
+      }
+      d = wave_sum_halves(d);
+      if (i == 0) del0 = d;
+      dd[qb][i] = del0 - d;
+      f_lse[qb][i] = seed_frag<E>(lse, hf);
+      if (rowok && hf == 0) p.delta[rs + i * bstride] = i == 0 ? -d : del0 - d;
+      float w = (rowok && hf == 0) ? d : 0.f;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) w += __shfl_xor(w, o, 64);
+      const int blk = qw0 + 32 * qb;
+      if (p.dcoef_part) {
+        if (lane == 0 && blk < T) p.dcoef_part[(((int64_t)hh * p.cst + i) * p.B + b) * ((T + 31) / 32) + blk / 32] = w;
+      } else if (lane == 0 && blk < T) {
+        atomicAdd(p.dcoef + hh * p.cst + i, w);
+      }
+    }
+    f_dp[qb] = seed_frag<E>(-del0, hf);
+  }
+
+#pragma unroll
+  for (int i = 0; i < N; ++i) stage<E, HS, BM, HS, NTHR>(Qs + i * BM * HS, gq + i * p.q.si, p.q.st, q0, T - 1, tid);
+  const int tile_pieces = KR::pieces(wave);
+  for (int j = 0; j < NS - 1; ++j)
+    if (j < ntiles) stage_kv(j, j);
+  wait_vm(tile_pieces * max(0, min(NS - 1, ntiles) - 1));
+  lds_barrier();
+  scale_lds<E, NTHR>(Qs, CF::nQ, p.sl2, tid);
+  lds_barrier();
+
+  f32x16 dq[2][N][NHB];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+#pragma unroll
+      for (int d = 0; d < NHB; ++d) dq[qb][i][d] = f32x16{};
+
+  int LrV = row_lane<VROWB>(lane), LrK = row_lane<ROWB>(lane), LtK = tr_lane<ROWB>(lane);
+
+  // one tile: the MFMA stream with the VALU pieces in its slots
+  auto body = [&](int kt, auto MASKED) {
+    constexpr bool MASK = decltype(MASKED)::value;
+    asm volatile("" : "+v"(LrV), "+v"(LrK), "+v"(LtK));
+    // the seed MFMAs are loop-invariant: keep them in the tile (an opaque "ones" operand),
+    // or the compiler hoists their results and copies 16 registers back per use
+    frag one = f_one;
+    asm volatile("" : "+v"(one));
+    const int buf = kt % NS, k0 = kt * BN;
+    const unsigned kbase = lds_addr(Kb + buf * CF::nK), vbase = lds_addr(Vb + buf * CF::nV);
+    const unsigned bK = LrK + kbase, tK = LtK + kbase, bV = LrV + vbase;
+    const unsigned bQ = LrK + lds_addr(Qs) + wave * 64 * ROWB;
+    int lim[2];
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) lim[qb] = min(qw0 + 32 * qb + (lane & 31), T - 1) - k0 - 4 * (lane >> 5);
+    f32x16 dp[2][NKB], sa[2][NKB];
+    frag pk[U][NKB * 2];
+    constexpr int RBN = R + 3, RQN = R / 2 + 2, RTN = R / 2 + 2;
+    i32x4 rb[RBN], rq[RQN];
+    lds64 rt[RTN][4];
+    auto issue = [&](auto S_) {
+      constexpr int s = decltype(S_)::value;
+      constexpr dq2::Op o = SCH::v.ops[s];
+      if constexpr (o.kind == dq2::SC) {
+        ds128<o.i * BN * ROWB + o.b * 32 * ROWB>(rb[SCH::v.rid[s] % RBN], bK ^ (32 * o.a));
+        if constexpr (o.b == 0) ds128<o.i * BM * ROWB + o.qb * 32 * ROWB>(rq[SCH::v.qid[s] % RQN], bQ ^ (32 * o.a));
+      } else if constexpr (o.kind == dq2::DC) {
+        ds128<o.b * 32 * VROWB>(rb[SCH::v.rid[s] % RBN], bV ^ (32 * o.a));
+      } else if constexpr (o.kind == dq2::CC && o.c == 0) {
+        tr_issue<ROWB, 32 * o.b, o.i * BN * ROWB>(rt[SCH::v.tid[s] % RTN], tK ^ (64 * o.a), tK ^ (64 * o.a + 32));
+      }
+    };
+    auto piece = [&](auto PU) {
+      constexpr int u = decltype(PU)::value / dq2::PIECES, j = decltype(PU)::value % dq2::PIECES;
+      constexpr int i = dq2::Sched<N, NSQ, NSV, NHB>::ui(u), qb = dq2::Sched<N, NSQ, NSV, NHB>::uq(u);
+      constexpr int kb = j / 8, r0 = (j % 8) * 2, sr = u % 2;
+#pragma unroll
+      for (int r = r0; r < r0 + 2; ++r) {
+        float arg = sa[sr][kb][r];
+        if constexpr (MASK) arg = (kb * 32 + (r & 3) + 8 * (r >> 2) > lim[qb]) ? -INFINITY : arg;
+        const float pr = exp2_fast(arg);
+        sa[sr][kb][r] = i == 0 ? pr * dp[qb][kb][r] : pr * (dp[qb][kb][r] + dd[qb][i]);
+      }
+      if constexpr (j % 4 == 3) pk[u][kb * 2 + (j % 8) / 4] = O::template pack<(j % 8) / 4>(sa[sr][kb]);
+    };
+    sfor<(R < NOPS ? R : NOPS)>([&](auto S_) { issue(S_); });
+    sfor<NOPS>([&](auto S_) {
+      constexpr int s = decltype(S_)::value;
+      constexpr dq2::Op o = SCH::v.ops[s];
+      if constexpr (s + R < NOPS) issue(std::integral_constant<int, s + R>{});
+      if constexpr (SCH::v.nreads[s] > 0) lgkm_wait<SCH::v.pending(s, R)>();
+      if constexpr (o.kind == dq2::SS) {
+        sa[o.u % 2][o.b] = O::mma(one, f_lse[o.qb][o.i], f32x16{});
+      } else if constexpr (o.kind == dq2::SC) {
+        i32x4& kr = rb[SCH::v.rid[s] % RBN];
+        i32x4& qr = rq[(o.b == 0 ? SCH::v.qid[s] : SCH::v.qid[s - 1]) % RQN];
+        asm volatile("" : "+v"(kr), "+v"(qr));
+        sa[o.u % 2][o.b] = O::mma(__builtin_bit_cast(frag, kr), __builtin_bit_cast(frag, qr), sa[o.u % 2][o.b]);
+      } else if constexpr (o.kind == dq2::DS) {
+        dp[o.qb][o.b] = O::mma(one, f_dp[o.qb], f32x16{});
+      } else if constexpr (o.kind == dq2::DC) {
+        i32x4& vr = rb[SCH::v.rid[s] % RBN];
+        asm volatile("" : "+v"(vr));
+        dp[o.qb][o.b] = O::mma(__builtin_bit_cast(frag, vr), df[o.qb][o.a], dp[o.qb][o.b]);
+      } else {
+        lds64 (&tr)[4] = rt[(o.c == 0 ? SCH::v.tid[s] : SCH::v.tid[s - 1]) % RTN];
+        if constexpr (o.c == 0) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(tr[j]));
+        }
+        mfma_agpr<(s == SCH::v.c0[o.u])>(dq[o.qb][o.i][o.a], tr_frag<E>(tr, o.c), pk[o.u][o.b * 2 + o.c]);
+      }
+      sfor<SCH::v.npiece[s]>([&](auto K) { piece(std::integral_constant<int, SCH::v.pu[s][decltype(K)::value]>{}); });
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  };
+  auto step = [&](int kt, auto MASKED, bool live) {
+    if (kt + NS - 1 < ntiles) stage_kv(kt + NS - 1, (kt + NS - 1) % NS);
+    if (live) body(kt, MASKED);
+    wait_vm(tile_pieces * max(0, min(NS - 2, ntiles - 2 - kt)));
+    lds_barrier();
+  };
+  // per wave: tiles wholly below its first row, its diagonal / ragged tiles, then tiles past
+  // its last row (DMA share and barrier only)
+  const bool wave_live = qw0 < T;
+  const int nfull = wave_live ? min(ntiles, min(qw0 / BN, T / BN)) : 0;
+  const int nlive = wave_live ? min(ntiles, qw0 / BN + 1) : 0;
+  for (int kt = 0; kt < nfull; ++kt) step(kt, std::false_type{}, true);
+  for (int kt = nfull; kt < nlive; ++kt) step(kt, std::true_type{}, true);
+  for (int kt = nlive; kt < ntiles; ++kt) step(kt, std::false_type{}, false);
+  dq2_acc_fence();
+
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const int qrow = qw0 + 32 * qb + c32;
+    if (qrow >= T) continue;
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+#pragma unroll
+      for (int d = 0; d < NHB; ++d)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int e = d * 32 + 8 * g + 4 * hf;
+          const float sc = p.scale * coef[i];
+          float a0 = dq[qb][i][d][4 * g] * sc, a1 = dq[qb][i][d][4 * g + 1] * sc;
+          float a2 = dq[qb][i][d][4 * g + 2] * sc, a3 = dq[qb][i][d][4 * g + 3] * sc;
+          if (p.rope) rope_inv4(p.rope, qrow, HS, e, a0, a1, a2, a3);
+          if (p.dq32) {
+            store4<float>(p.dq32 + ((((int64_t)b * T + qrow) * p.H + hh) * p.cst + i) * HS + e, a0, a1, a2, a3);
+          } else {
+            E* gdq = reinterpret_cast<E*>(p.dq.p) + b * p.dq.sb + (int64_t)qrow * p.dq.st + hh * p.dq.sh + i * p.dq.si;
+            store4<E>(gdq + e, a0, a1, a2, a3);
+          }
+        }
+  }
+}
+
 // One query tile of the key-major backward -- Q_i rows, dO rows, LSE rows and
 // (with DELTA) c*delta rows -- streamed into one ring stage by buffer_load ... lds.
 // Stage layout: [N][BQ][HSP] Q image | [BQ][DVP] dO image | [NP] lse | [NP] c*delta
@@ -2091,6 +2480,24 @@ int launch_fwd_t(const FwdParams& p, hipStream_t st) {
   }
 }
 
+int launch_attn_dq2_bf16(const BwdParams& p, hipStream_t st);   // attn_bf16_dq2.hip
+template <class E, int HS, int N, int DV>
+int launch_dq2_t(const BwdParams& p, hipStream_t st) {
+  using C2 = Dq2Cfg<E, HS, N, DV>;
+  auto kern = attn_dq2_kernel<E, HS, N, DV>;
+  if (int e = set_smem(kern, C2::bytes)) return e;
+  hipLaunchKernelGGL(kern, dim3((p.T + C2::BM - 1) / C2::BM, p.H, p.B), dim3(256), C2::bytes, st, p);
+  return (int)hipGetLastError();
+}
+// DTA_DQ2 = 0 in the environment keeps attn_dq_kernel where attn_dq2_kernel is built (A/B)
+static inline bool dq2_env() {
+  static const bool v = [] {
+    const char* s = getenv("DTA_DQ2");
+    return !(s && *s == '0');
+  }();
+  return v;
+}
+
 template <class E, int HS, int N, int DV_, bool DROP>
 int launch_dq_t(const BwdParams& p, hipStream_t st) {
   using PL = Plan<E, HS, N, DV_>;
@@ -2101,6 +2508,11 @@ int launch_dq_t(const BwdParams& p, hipStream_t st) {
   constexpr bool B32 = DP::B32;
   using CF = DqCfg<E, HS, N, DV, NW, QR, QH, B32>;
   constexpr int bytes = CF::bytes;
+  if constexpr (Dq2Cfg<E, HS, N, DV>::ok && !DROP && KvRing<E, HS, N, DV, 64, 4>::ok) {
+    // one wave per SIMD, two 32-row blocks per wave (attn_dq2_kernel, its own unit:
+    // attn_bf16_dq2.hip)
+    if (kv_layout_ok(p, (int)sizeof(E)) && dq2_env()) return launch_attn_dq2_bf16(p, st);
+  }
   dim3 grid((p.T + NW * 32 - 1) / (NW * 32), p.H, p.B);
   auto run = [&](auto F32, auto SRDV) -> int {
     auto kern = attn_dq_kernel<E, HS, N, DV, NW, QR, decltype(F32)::value, decltype(SRDV)::value, DROP, QH, B32>;
