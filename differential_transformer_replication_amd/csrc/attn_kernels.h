@@ -1717,6 +1717,16 @@ void attn_dq2_kernel(BwdParams p) {
     }
     f_dp[qb] = seed_frag<E>(-del0, hf);
   }
+  // loop-invariant MFMA operands (the dO rows, the seed fragments) pinned to AGPRs: MFMAs
+  // read A / B operands from either half, and the VGPRs go to the values the VALU touches
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+#pragma unroll
+    for (int s = 0; s < NSV; ++s) asm volatile("" : "+a"(df[qb][s]));
+#pragma unroll
+    for (int i = 0; i < N; ++i) asm volatile("" : "+a"(f_lse[qb][i]));
+    asm volatile("" : "+a"(f_dp[qb]));
+  }
 
 #pragma unroll
   for (int i = 0; i < N; ++i) stage<E, HS, BM, HS, NTHR>(Qs + i * BM * HS, gq + i * p.q.si, p.q.st, q0, T - 1, tid);
@@ -2363,6 +2373,374 @@ void attn_dkdv_kernel(BwdParams p) {
   }
 }
 
+// --------------------------- backward: dK, dV, two query sub-blocks per step ---
+// attn_dkdv2_kernel: attn_dkdv_kernel re-planned like attn_dq2_kernel -- one wave per SIMD,
+// 4 waves x 32 keys = 128 keys per workgroup, 64-row query steps (two 32-row sub-blocks
+// per step from a TileRing<BQ = 64> LDS-DMA ring).  The wave's own K_i rows (prescaled by
+// sl2) and V rows are loop-invariant MFMA operands: loaded once into AGPRs.  dK_i and dV
+// accumulate in AGPRs (mfma_agpr).  Each step is a compile-time MFMA stream -- per unit
+// u = (branch, sub-block) the S' chain seeded with the -LSE rows, per sub-block the dP chain
+// seeded with -delta_0 (and, for branches i >= 1, one more seeded MFMA adding
+// delta_0 - delta_i), the dK_i and dV products -- with each unit's exp / dS / combined-P
+// VALU placed into the slots of MFMAs that do not depend on it (Kv2Sched).
+namespace kv2 {
+enum : int { SS = 0, SC = 1, DS = 2, DC = 3, XS = 4, CK = 5, CV = 6 };
+struct Op { int kind = 0, u = 0, qs = 0, i = 0, a = 0, c = 0; };
+constexpr int PIECES = 8;      // VALU pieces per unit: 16 elements, two at a time
+
+template <int N, int NSQ, int NSV, int NHB, int NVB>
+struct Sched {
+  static constexpr int U = 2 * N, SR = 2;
+  static constexpr int NOPS = U * (1 + NSQ) + 2 * (1 + NSV) + 2 * (N - 1) + U * NHB * 2 + 2 * NVB * 2;
+  static constexpr int ui(int u) { return N - 1 - u / 2; }
+  static constexpr int uq(int u) { return u % 2; }
+  static constexpr bool first_of_qs(int u) { return u < 2; }        // branch N-1: pc starts here
+  static constexpr bool last_of_qs(int u) { return u >= U - 2; }    // branch 0: pc complete
+  Op ops[NOPS];
+  int s0[U] = {}, s1[U] = {}, c0[U] = {}, d1[2] = {}, x1[U] = {}, v0[2] = {};
+  int E[U] = {}, Dl[U] = {};
+  int npiece[NOPS] = {};
+  int pu[NOPS][PIECES * 4] = {};
+  int nreads[NOPS] = {};
+  int rid[NOPS] = {};          // b128 reads (Q / dO fragments)
+  int tid[NOPS] = {};          // tr blocks (dK: Q^T, dV: dO^T)
+  bool ok = true;
+  constexpr Op mk(int kind, int u, int qs, int i, int a, int c) const {
+    Op o; o.kind = kind; o.u = u; o.qs = qs; o.i = i; o.a = a; o.c = c; return o;
+  }
+  constexpr void add_s(int& n, int u) {
+    s0[u] = n;
+    ops[n++] = mk(SS, u, uq(u), ui(u), 0, 0);
+    for (int st = 0; st < NSQ; ++st) ops[n++] = mk(SC, u, uq(u), ui(u), st, 0);
+    s1[u] = n - 1;
+  }
+  constexpr void add_d(int& n, int qs) {
+    ops[n++] = mk(DS, 0, qs, 0, 0, 0);
+    for (int s = 0; s < NSV; ++s) ops[n++] = mk(DC, 0, qs, 0, s, 0);
+    d1[qs] = n - 1;
+    for (int u = 0; u < U; ++u)
+      if (uq(u) == qs && ui(u) >= 1) { ops[n] = mk(XS, u, qs, ui(u), 0, 0); x1[u] = n++; }
+  }
+  constexpr void add_ck(int& n, int u) {
+    c0[u] = n;
+    for (int d = 0; d < NHB; ++d)
+      for (int ks = 0; ks < 2; ++ks) ops[n++] = mk(CK, u, uq(u), ui(u), d, ks);
+  }
+  constexpr void add_cv(int& n, int qs) {
+    v0[qs] = n;
+    for (int d = 0; d < NVB; ++d)
+      for (int ks = 0; ks < 2; ++ks) ops[n++] = mk(CV, 0, qs, 0, d, ks);
+  }
+  constexpr Sched() {
+    int n = 0;
+    add_s(n, 0); add_d(n, 0);
+    add_s(n, 1); add_d(n, 1);
+    for (int u = 2; u < U; ++u) { add_s(n, u); add_ck(n, u - 2); }
+    add_ck(n, U - 2); add_cv(n, 0);
+    add_ck(n, U - 1); add_cv(n, 1);
+    if (n != NOPS) ok = false;
+    for (int u = 0; u < U; ++u) {
+      int e = s1[u] > d1[uq(u)] ? s1[u] : d1[uq(u)];
+      if (ui(u) >= 1 && x1[u] > e) e = x1[u];
+      E[u] = e + 1;
+      Dl[u] = c0[u] - 1;
+      if (last_of_qs(u) && v0[uq(u)] - 1 < Dl[u]) Dl[u] = v0[uq(u)] - 1;
+      if (u + SR < U && s0[u + SR] < Dl[u]) Dl[u] = s0[u + SR];
+      // the next unit of the same sub-block accumulates into the same combined P: keep order
+    }
+    int load[NOPS] = {};
+    int prev_end[2] = {0, 0};
+    for (int u = 0; u < U; ++u) {
+      const int lo = E[u] > prev_end[uq(u)] ? E[u] : prev_end[uq(u)];
+      int cap = 1;
+      for (;; ++cap) {
+        int room = 0;
+        for (int x = lo; x < Dl[u]; ++x) room += load[x] < cap ? cap - load[x] : 0;
+        if (room >= PIECES || cap >= PIECES * 4) break;
+      }
+      int j = 0, last = lo;
+      for (int x = lo; x < Dl[u] && j < PIECES; ++x)
+        while (load[x] < cap && j < PIECES) {
+          if (npiece[x] < PIECES * 4) pu[x][npiece[x]++] = u * PIECES + j; else ok = false;
+          ++load[x];
+          ++j;
+          last = x;
+        }
+      if (j < PIECES) ok = false;
+      prev_end[uq(u)] = last;
+    }
+    int nb = 0, ntr = 0;
+    for (int s = 0; s < NOPS; ++s) {
+      const Op& o = ops[s];
+      if (o.kind == SC || o.kind == DC) { rid[s] = nb++; nreads[s] = 1; }
+      else if ((o.kind == CK || o.kind == CV) && o.c == 0) { tid[s] = ntr++; nreads[s] = 4; }
+    }
+  }
+  constexpr int pending(int s, int R) const {
+    int c = 0;
+    for (int x = s + 1; x <= s + R && x < NOPS; ++x) c += nreads[x];
+    return c;
+  }
+};
+template <int N, int NSQ, int NSV, int NHB, int NVB>
+struct Hold { static constexpr Sched<N, NSQ, NSV, NHB, NVB> v{}; };
+}  // namespace kv2
+
+#ifndef DTA_DKDV2
+#define DTA_DKDV2 1
+#endif
+template <class E, int HS, int N, int DV>
+struct Kv2Cfg {
+  static constexpr int NW = 4, BK = 128, BQ = 64;
+  using RG = TileRing<E, HS, N, DV, NW, true, BQ, true>;
+  static constexpr int NS = (160 * 1024) / RG::SB >= 4 ? 4 : ((160 * 1024) / RG::SB >= 3 ? 3 : 2);
+  static constexpr int bytes = NS * RG::SB;
+  static constexpr int NHB = HS / 32, NVB = DV / 32;
+  // VGPRs: dP (2 sub-blocks) + the branch-corrected dP of branches >= 1, two S' sets, packed
+  // dS of every unit, combined P and its packs, seeds, read buffers; AGPRs: dK, dV, K, V
+  static constexpr int vregs = 2 * 16 + 2 * (N - 1) * 16 + 2 * 16 + 2 * N * 8 + 2 * 16 + 2 * 8 + 4 * N * 4 + 80;
+  static constexpr int aregs = N * NHB * 16 + NVB * 16 + N * HS / 4 + DV / 4 + 4;
+  static constexpr bool shape_ok = DTA_DKDV2 && std::is_same<E, __bf16>::value && (HS == 32 || HS == 64 || HS == 128) &&
+                                   (DV == HS || DV == 2 * HS) && DV <= 128 && RG::ok && 2 * RG::SB <= 160 * 1024 &&
+                                   vregs <= 256 && aregs <= 256;
+  template <bool S, int = 0> struct Sok { static constexpr bool v = false; };
+  template <int X> struct Sok<true, X> { static constexpr bool v = kv2::Hold<N, HS / 16, DV / 16, HS / 32, DV / 32>::v.ok; };
+  static constexpr bool ok = Sok<shape_ok>::v;
+};
+
+template <class E, int HS, int N, int DV>
+__global__ __launch_bounds__(256, 1)
+void attn_dkdv2_kernel(BwdParams p) {
+  using O = Ops<E>;
+  using frag = typename O::frag;
+  using CF = Kv2Cfg<E, HS, N, DV>;
+  using RG = typename CF::RG;
+  constexpr int NW = CF::NW, BK = CF::BK, BQ = CF::BQ, KS = O::KSTEP, NS = CF::NS;
+  constexpr int NSQ = HS / KS, NSV = DV / KS, NHB = HS / 32, NVB = DV / 32;
+  constexpr int QROWB = RG::HSP * (int)sizeof(E), DROWB = RG::DVP * (int)sizeof(E);
+  constexpr int R = DTA_DQ2_R;
+  using SCH = kv2::Hold<N, NSQ, NSV, NHB, NVB>;
+  using SD = kv2::Sched<N, NSQ, NSV, NHB, NVB>;
+  constexpr int NOPS = SD::NOPS, U = 2 * N;
+  static_assert(SCH::v.ok, "dK/dV2 schedule");
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* ringb = smem;                     // NS stages of TileRing<BQ = 64>
+
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int tid = threadIdx.x, lane = tid & 63;
+  int hf = lane >> 5, c32 = lane & 31;
+  int bx, by, bz, lin;
+  lpt_order(bx, by, bz, lin);
+  const int kblk = bx;
+  const int hh = by, b = bz;
+  const int T = p.T;
+  const int kb0 = kblk * BK, kw0 = kb0 + wave * 32;
+  const int krow = kw0 + c32;
+  const E* gq = reinterpret_cast<const E*>(p.q.p) + b * p.q.sb + hh * p.q.sh;
+  const E* gk = reinterpret_cast<const E*>(p.k.p) + b * p.k.sb + hh * p.k.sh;
+  const E* gv = reinterpret_cast<const E*>(p.v.p) + b * p.v.sb + hh * p.v.sh;
+  const E* gdo = reinterpret_cast<const E*>(p.dout.p) + b * p.dout.sb + hh * p.dout.sh;
+  const int64_t rowvec = ((int64_t)b * p.H + hh) * T;
+  const int64_t bstride = (int64_t)p.B * p.H * T;
+
+  float coef[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) coef[i] = p.coef[hh * p.cst + i];
+  // this wave's K_i rows (x sl2) and V rows: B operands of S' and dP, in AGPRs
+  frag kf[N][NSQ], vf[NSV];
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+#pragma unroll
+    for (int st = 0; st < NSQ; ++st) {
+      frag f = krow < T ? O::load_global(gk + (int64_t)krow * p.k.st + i * p.k.si + st * KS + hf * O::KH) : O::zero();
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = (E)((float)f[j] * p.sl2);
+      kf[i][st] = f;
+    }
+#pragma unroll
+  for (int s = 0; s < NSV; ++s)
+    vf[s] = krow < T ? O::load_global(gv + (int64_t)krow * p.v.st + s * KS + hf * O::KH) : O::zero();
+  frag f_one = O::zero();
+  if (hf == 0) { f_one[0] = (E)1.f; f_one[1] = (E)1.f; }
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+#pragma unroll
+    for (int st = 0; st < NSQ; ++st) asm volatile("" : "+a"(kf[i][st]));
+#pragma unroll
+  for (int s = 0; s < NSV; ++s) asm volatile("" : "+a"(vf[s]));
+
+  uint32_t roff[RG::MYP];
+  RG::offsets(p, bstride, wave, lane, roff);
+  const int nsteps = kb0 < T ? (T - kb0 + BQ - 1) / BQ : 0;
+  auto stage_q = [&](int q0, int buf) {
+    RG::issue_pre(p, gq, gdo, p.lse + rowvec, p.delta + rowvec, bstride, q0, T, ringb + buf * RG::SB, wave, roff);
+  };
+  const int tile_pieces = RG::pieces(wave);
+  for (int j = 0; j < NS - 1; ++j)
+    if (j < nsteps) stage_q(kb0 + j * BQ, j);
+  wait_vm(tile_pieces * max(0, min(NS - 1, nsteps) - 1));
+  lds_barrier();
+
+  f32x16 dk[N][NHB], dv[NVB];
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+#pragma unroll
+    for (int d = 0; d < NHB; ++d) dk[i][d] = f32x16{};
+#pragma unroll
+  for (int d = 0; d < NVB; ++d) dv[d] = f32x16{};
+
+  int LrQ = row_lane<QROWB>(lane), LrD = row_lane<DROWB>(lane), LtQ = tr_lane<QROWB>(lane), LtD = tr_lane<DROWB>(lane);
+
+  auto body = [&](int t, auto MASKED) {
+    constexpr bool MASK = decltype(MASKED)::value;
+    asm volatile("" : "+v"(LrQ), "+v"(LrD), "+v"(LtQ), "+v"(LtD));
+    frag one = f_one;
+    asm volatile("" : "+v"(one));
+    const int buf = t % NS, qs0 = kb0 + t * BQ;
+    const char* sg = ringb + buf * RG::SB;
+    const unsigned sb = lds_addr(sg);
+    const unsigned bQ = LrQ + sb, bD = LrD + sb, tQ = LtQ + sb, tD = LtD + sb;
+    const float* Lc = reinterpret_cast<const float*>(sg + RG::OFF_L);
+    const float* Gc = reinterpret_cast<const float*>(sg + RG::OFF_G);
+    // row seeds (row = query = lane & 31 of an A operand): -LSE_i, -delta_0, delta_0 - delta_i
+    frag sseed[N][2], dseed[2], xseed[N > 1 ? N : 2][2];
+#pragma unroll
+    for (int qs = 0; qs < 2; ++qs) {
+      const int r = 32 * qs + (lane & 31);
+#pragma unroll
+      for (int i = 0; i < N; ++i) sseed[i][qs] = seed_frag<E>(Lc[i * BQ + r], lane >> 5);
+      dseed[qs] = seed_frag<E>(Gc[r], lane >> 5);
+#pragma unroll
+      for (int i = 1; i < N; ++i) xseed[i][qs] = seed_frag<E>(Gc[i * BQ + r], lane >> 5);
+    }
+    int lim_lo[2], lim_hi[2];
+#pragma unroll
+    for (int qs = 0; qs < 2; ++qs) {
+      lim_lo[qs] = krow - (qs0 + 32 * qs) - 4 * (lane >> 5);
+      lim_hi[qs] = T - 1 - (qs0 + 32 * qs) - 4 * (lane >> 5);
+    }
+    f32x16 dpa[2], dpx[U > 2 ? U : 1], sa[2], pc[2];
+    frag dsp[U][2], pcp[2][2];
+    constexpr int RBN = R + 1, RTN = (R + 1) / 2 + 1;
+    i32x4 rb[RBN];
+    lds64 rt[RTN][4];
+    auto issue = [&](auto S_) {
+      constexpr int s = decltype(S_)::value;
+      constexpr kv2::Op o = SCH::v.ops[s];
+      if constexpr (o.kind == kv2::SC) {
+        ds128<o.i * RG::QB + o.qs * 32 * QROWB>(rb[SCH::v.rid[s] % RBN], bQ ^ (32 * o.a));
+      } else if constexpr (o.kind == kv2::DC) {
+        ds128<RG::OFF_D + o.qs * 32 * DROWB>(rb[SCH::v.rid[s] % RBN], bD ^ (32 * o.a));
+      } else if constexpr (o.kind == kv2::CK && o.c == 0) {
+        tr_issue<QROWB, 32 * o.qs, o.i * RG::QB>(rt[SCH::v.tid[s] % RTN], tQ ^ (64 * o.a), tQ ^ (64 * o.a + 32));
+      } else if constexpr (o.kind == kv2::CV && o.c == 0) {
+        tr_issue<DROWB, 32 * o.qs, RG::OFF_D>(rt[SCH::v.tid[s] % RTN], tD ^ (64 * o.a), tD ^ (64 * o.a + 32));
+      }
+    };
+    auto piece = [&](auto PU) {
+      constexpr int u = decltype(PU)::value / kv2::PIECES, j = decltype(PU)::value % kv2::PIECES;
+      constexpr int i = SD::ui(u), qs = SD::uq(u), su = u % 2;
+#pragma unroll
+      for (int r = 2 * j; r < 2 * j + 2; ++r) {
+        float arg = sa[su][r];
+        if constexpr (MASK) {
+          const int rc = (r & 3) + 8 * (r >> 2);
+          arg = (rc < lim_lo[qs] || rc > lim_hi[qs]) ? -INFINITY : arg;
+        }
+        const float pr = exp2_fast(arg);
+        if constexpr (SD::first_of_qs(u)) pc[qs][r] = coef[i] * pr;
+        else pc[qs][r] = fmaf(coef[i], pr, pc[qs][r]);
+        sa[su][r] = pr * (i == 0 ? dpa[qs][r] : dpx[U > 2 ? u : 0][r]);
+      }
+      if constexpr (j % 4 == 3) {
+        dsp[u][j / 4] = O::template pack<j / 4>(sa[su]);
+        if constexpr (SD::last_of_qs(u)) pcp[qs][j / 4] = O::template pack<j / 4>(pc[qs]);
+      }
+    };
+    sfor<(R < NOPS ? R : NOPS)>([&](auto S_) { issue(S_); });
+    sfor<NOPS>([&](auto S_) {
+      constexpr int s = decltype(S_)::value;
+      constexpr kv2::Op o = SCH::v.ops[s];
+      if constexpr (s + R < NOPS) issue(std::integral_constant<int, s + R>{});
+      if constexpr (SCH::v.nreads[s] > 0) lgkm_wait<SCH::v.pending(s, R)>();
+      if constexpr (o.kind == kv2::SS) {
+        sa[o.u % 2] = O::mma(sseed[o.i][o.qs], one, f32x16{});
+      } else if constexpr (o.kind == kv2::SC) {
+        i32x4& qr = rb[SCH::v.rid[s] % RBN];
+        asm volatile("" : "+v"(qr));
+        sa[o.u % 2] = O::mma(__builtin_bit_cast(frag, qr), kf[o.i][o.a], sa[o.u % 2]);
+      } else if constexpr (o.kind == kv2::DS) {
+        dpa[o.qs] = O::mma(dseed[o.qs], one, f32x16{});
+      } else if constexpr (o.kind == kv2::DC) {
+        i32x4& dr = rb[SCH::v.rid[s] % RBN];
+        asm volatile("" : "+v"(dr));
+        dpa[o.qs] = O::mma(__builtin_bit_cast(frag, dr), vf[o.a], dpa[o.qs]);
+      } else if constexpr (o.kind == kv2::XS) {
+        dpx[U > 2 ? o.u : 0] = O::mma(xseed[o.i][o.qs], one, dpa[o.qs]);
+      } else {
+        lds64 (&tr)[4] = rt[(o.c == 0 ? SCH::v.tid[s] : SCH::v.tid[s - 1]) % RTN];
+        if constexpr (o.c == 0) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(tr[j]));
+        }
+        if constexpr (o.kind == kv2::CK)
+          mfma_agpr<(s == SCH::v.c0[o.u])>(dk[o.i][o.a], tr_frag<E>(tr, o.c), dsp[o.u][o.c]);
+        else
+          mfma_agpr<(s == SCH::v.v0[o.qs])>(dv[o.a], tr_frag<E>(tr, o.c), pcp[o.qs][o.c]);
+      }
+      sfor<SCH::v.npiece[s]>([&](auto K) { piece(std::integral_constant<int, SCH::v.pu[s][decltype(K)::value]>{}); });
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  };
+  auto step = [&](int t, auto MASKED, bool live) {
+    if (t + NS - 1 < nsteps) stage_q(kb0 + (t + NS - 1) * BQ, (t + NS - 1) % NS);
+    if (live) body(t, MASKED);
+    wait_vm(tile_pieces * max(0, min(NS - 2, nsteps - 2 - t)));
+    lds_barrier();
+  };
+  // per wave: steps wholly before its first key (nothing to add), its diagonal steps,
+  // the unmasked middle, a ragged tail step
+  const bool wave_keys = kw0 < T;
+  const int tlive = wave_keys ? min(nsteps, (kw0 - kb0) / BQ) : nsteps;
+  const int tfull = wave_keys ? min(nsteps, (kw0 - kb0 + 31 + BQ - 1) / BQ) : nsteps;
+  const int ttail = wave_keys ? max(tfull, nsteps - ((T - kb0) % BQ != 0 ? 1 : 0)) : nsteps;
+  for (int t = 0; t < tlive; ++t) step(t, std::false_type{}, false);
+  for (int t = tlive; t < tfull; ++t) step(t, std::true_type{}, true);
+  for (int t = tfull; t < ttail; ++t) step(t, std::false_type{}, true);
+  for (int t = ttail; t < nsteps; ++t) step(t, std::true_type{}, true);
+  dq2_acc_fence();
+
+  if (!wave_keys || krow >= T) return;
+  E* gdk = reinterpret_cast<E*>(p.dk.p) + b * p.dk.sb + (int64_t)krow * p.dk.st + hh * p.dk.sh;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const float sc = p.scale * coef[i];
+#pragma unroll
+    for (int d = 0; d < NHB; ++d)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int e = d * 32 + 8 * g + 4 * hf;
+        float a0 = dk[i][d][4 * g] * sc, a1 = dk[i][d][4 * g + 1] * sc;
+        float a2 = dk[i][d][4 * g + 2] * sc, a3 = dk[i][d][4 * g + 3] * sc;
+        if (p.rope) rope_inv4(p.rope, krow, HS, e, a0, a1, a2, a3);
+        store4<E>(gdk + i * p.dk.si + e, a0, a1, a2, a3);
+      }
+  }
+  E* gdv = reinterpret_cast<E*>(p.dv.p) + b * p.dv.sb + (int64_t)krow * p.dv.st + hh * p.dv.sh;
+#pragma unroll
+  for (int d = 0; d < NVB; ++d)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int e = d * 32 + 8 * g + 4 * hf;
+      float a0 = dv[d][4 * g], a1 = dv[d][4 * g + 1], a2 = dv[d][4 * g + 2], a3 = dv[d][4 * g + 3];
+      if (p.dv_acc) {
+        a0 += (float)gdv[e]; a1 += (float)gdv[e + 1]; a2 += (float)gdv[e + 2]; a3 += (float)gdv[e + 3];
+      }
+      store4<E>(gdv + e, a0, a1, a2, a3);
+    }
+}
+
 // ------------------------------------------------------------ launchers ---
 template <class K>
 static inline int set_smem(K kernel, int bytes) {
@@ -2481,6 +2859,23 @@ int launch_fwd_t(const FwdParams& p, hipStream_t st) {
 }
 
 int launch_attn_dq2_bf16(const BwdParams& p, hipStream_t st);   // attn_bf16_dq2.hip
+int launch_attn_dkdv2_bf16(const BwdParams& p, hipStream_t st); // attn_bf16_dq2.hip
+template <class E, int HS, int N, int DV>
+int launch_dkdv2_t(const BwdParams& p, hipStream_t st) {
+  using C2 = Kv2Cfg<E, HS, N, DV>;
+  auto kern = attn_dkdv2_kernel<E, HS, N, DV>;
+  if (int e = set_smem(kern, C2::bytes)) return e;
+  hipLaunchKernelGGL(kern, dim3((p.T + C2::BK - 1) / C2::BK, p.H, p.B), dim3(256), C2::bytes, st, p);
+  return (int)hipGetLastError();
+}
+// DTA_DKDV2 = 0 in the environment keeps attn_dkdv_kernel where attn_dkdv2_kernel is built
+static inline bool dkdv2_env() {
+  static const bool v = [] {
+    const char* s = getenv("DTA_DKDV2");
+    return !(s && *s == '0');
+  }();
+  return v;
+}
 template <class E, int HS, int N, int DV>
 int launch_dq2_t(const BwdParams& p, hipStream_t st) {
   using C2 = Dq2Cfg<E, HS, N, DV>;
@@ -2539,6 +2934,10 @@ int launch_dkdv_t(const BwdParams& p, hipStream_t st) {
   constexpr bool PR = KW::pair && !GR;
   using CF = DkdvCfg<E, HS, N, DV, NW, PR, GR>;
   constexpr int bytes = CF::bytes;
+  if constexpr (Kv2Cfg<E, HS, N, DV>::ok && !DROP) {
+    // one wave per SIMD, 64-row query steps (attn_dkdv2_kernel, its own unit: attn_bf16_dq2.hip)
+    if (ring_layout_ok(p, (int)sizeof(E)) && dkdv2_env()) return launch_attn_dkdv2_bf16(p, st);
+  }
   dim3 grid((p.T + NW * 32 - 1) / (NW * 32), p.H, p.B);
   dim3 block(NW * 64);
   // one-wave-per-SIMD 16-bit plans (4 waves, not paired) have 512 registers: dK and dV
