@@ -87,8 +87,8 @@ def test_module_bf16_autocast(golden, prefix):
         # heavy cancellation (d lambda = sum <dO, A_i V>) carries the bf16 rounding of its terms,
         # so the bar is the north star's 2e-2 or, where larger, 2x the error of the reference
         # algorithm itself under the same bf16 autocast (the oracle run on the GPU): the two
-        # round at different points (the reference rounds dO V^T per map element to bf16, the
-        # fused path rounds the per-branch outputs O_i that delta_i = <dO, O_i> is formed from).
+        # round at different points (the reference rounds dO V^T per map element to bf16; the
+        # fused path forms delta_i = <dO, O_i> from fp32 O_i but rounds P to bf16 for P V).
         ref_err = _reference_bf16_grad_errors(case, g)
         named = dict(m.named_parameters())
         log = []

@@ -121,7 +121,7 @@ def test_forced_rescale(dtype):
     q[:, :, :, 0] += 2.0 * u
     # branch-0 score of key 700 ~ 60/sqrt(hs) = 7.5 for every query: a jump of ~10 (log2 units)
     # over the running max, with P(key 700) ~ 0.7 -- not saturated, so dS = P(dP - delta) stays
-    # well conditioned under the bf16-stored O_i that delta is computed from
+    # well conditioned
     k[:, 700, :, 0] = 30.0 * u
     k[:, 333, 1, 1] = -40.0 * u           # a large negative outlier in the other branch
     coef = torch.tensor([[1.0, -0.4], [1.0, -0.6]])

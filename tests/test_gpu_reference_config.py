@@ -109,45 +109,30 @@ def test_default_config_diff_transformer_bf16_autocast():
     loss.backward()
     torch.cuda.synchronize()
     assert rel_err(logits.float().cpu(), ref_logits.detach()) < 2e-2
-    # Through two blocks of bf16 GEMMs and LayerNorms a weight gradient carries more than one
-    # bf16 rounding: the bar is 2e-2 or, where larger, 2x the error of the reference
-    # algorithm itself run under the same bf16 autocast (the oracle model on the GPU), as in
-    # test_gpu_modules.test_module_bf16_autocast; every error and bar is logged.
+    # Bars (north_star: bf16 <= 2e-2 on outputs and gradients): every attention parameter's
+    # gradient except the lambda vectors within 2e-2 of the fp64 oracle.  A lambda vector's
+    # gradient is a sum over B*T*dv terms that cancel (LayerNorm backward: <dX, X - mean> = 0
+    # per token across the heads; measured on the fp64 oracle for this seed, block 0 head 1:
+    # d(lambda) = 2.6e-4 against sum|terms| = 4.07, 1.6e4 : 1), so one bf16 rounding anywhere
+    # upstream moves it by O(1).  Each head's lambda gradient is therefore held, head by
+    # head, to 2x the error of the reference algorithm itself under the same bf16 autocast
+    # (the oracle model run on the GPU), at least 2e-2.  Every error and bar is logged.
     sd32 = {k: v.detach().float().to(DEV).requires_grad_(True) for k, v in sd.items()}
     with torch.autocast("cuda", dtype=torch.bfloat16):
         _, l32 = _oracle_diff_transformer(sd32, idx.to(DEV), tgt.to(DEV), 4, 2, 512)
     l32.backward()
-    # lambda vectors: one head's d(lambda) is a sum over B*T*dv terms that cancel (LayerNorm
-    # backward: <dX, X - mean> = 0 per token across the heads).  Measured on the fp64 oracle
-    # for this seed, block 0 head 1: d(lambda) = 2.6e-4 against sum|terms| = 4.07 (1.6e4 : 1),
-    # so one bf16 rounding anywhere upstream moves it by O(1) -- the reference algorithm under
-    # bf16 autocast is itself 0.28 off there.  Each lambda family of a module (e.g.
-    # lambda_q1 of all heads) is therefore scored as ONE tensor, max|a-b| / max|b| over its
-    # heads, like every other parameter; the per-head errors are logged.
-    log, fam = [], {}
+    log, bad = [], []
     for n, p in m.named_parameters():
         if ".diff_attn." not in n:
             continue
         got, ref, r32 = p.grad.double().cpu(), sd[n].grad, sd32[n].grad.double().cpu()
         err, ref_err = rel_err(got, ref), rel_err(r32, ref)
-        if ".lambda_" in n:
-            head_pre, leaf = n.rsplit(".heads.", 1)
-            key = head_pre + ".heads.*." + leaf.split(".", 1)[1]
-            fam.setdefault(key, []).append((got, ref, r32))
-            log.append({"param": n, "err": err, "ref_alg_bf16_err": ref_err, "scored": key})
-            continue
-        bar = max(2e-2, 2.0 * ref_err)
+        bar = max(2e-2, 2.0 * ref_err) if ".lambda_" in n else 2e-2
         log.append({"param": n, "err": err, "ref_alg_bf16_err": ref_err, "bar": bar})
-        assert err < bar, (n, err, ref_err)
-    for key, rows in fam.items():
-        got = torch.cat([r[0].flatten() for r in rows])
-        ref = torch.cat([r[1].flatten() for r in rows])
-        r32 = torch.cat([r[2].flatten() for r in rows])
-        err, ref_err = rel_err(got, ref), rel_err(r32, ref)
-        bar = max(2e-2, 2.0 * ref_err)
-        log.append({"param": key, "err": err, "ref_alg_bf16_err": ref_err, "bar": bar})
-        assert err < bar, (key, err, ref_err)
+        if not err < bar:
+            bad.append((n, err, ref_err, bar))
     _log("bf16_grad_errors_default_config_model", log)
+    assert not bad, bad
 
 
 @pytest.mark.parametrize("n_terms", [2, 3, 4])
