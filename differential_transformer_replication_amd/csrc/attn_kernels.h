@@ -3310,7 +3310,7 @@ int launch_fwd2_t(const FwdParams& p, hipStream_t st) {
 static inline bool fwd2_env() {
   static const bool v = [] {
     const char* s = getenv("DTA_FWD2");
-    return !(s && *s == '0');
+    return s && *s == '1';           // opt-in until verified on the GPU
   }();
   return v;
 }
@@ -3318,7 +3318,7 @@ static inline bool fwd2_env() {
 static inline bool dkdv2_env() {
   static const bool v = [] {
     const char* s = getenv("DTA_DKDV2");
-    return !(s && *s == '0');
+    return s && *s == '1';           // opt-in until verified on the GPU
   }();
   return v;
 }
@@ -3334,7 +3334,7 @@ int launch_dq2_t(const BwdParams& p, hipStream_t st) {
 static inline bool dq2_env() {
   static const bool v = [] {
     const char* s = getenv("DTA_DQ2");
-    return !(s && *s == '0');
+    return s && *s == '1';           // opt-in until verified on the GPU
   }();
   return v;
 }
