@@ -2299,21 +2299,26 @@ void attn_dkdv_kernel(BwdParams p) {
           const int Ld = LtD;
           const frag p0 = O::template pack<0>(pc), p1 = O::template pack<1>(pc);
           constexpr int NP2 = NVB >= 2 ? 2 : 1;       // d-blocks per LDS read batch
-          sfor<NVB / NP2>([&](auto D2) {
-            constexpr int d0 = NP2 * decltype(D2)::value;
-            lds64 r[NP2][4];
-            sfor<NP2>([&](auto E2) {
+          auto dv_blocks = [&](auto D0, auto NB) {
+            constexpr int d0 = decltype(D0)::value, nb = decltype(NB)::value;
+            lds64 r[nb][4];
+            sfor<nb>([&](auto E2) {
               constexpr int d = d0 + decltype(E2)::value;
               if constexpr (XA) tr_issue<DI::ROWB, 0, RG::OFF_D>(r[decltype(E2)::value], tD ^ (64 * d), tD ^ (64 * d + 32));
               else tr_issue<DI::ROWB, 0>(r[decltype(E2)::value], db + (Ld ^ (64 * d)), db + (Ld ^ (64 * d + 32)));
             });
-            lgkm_pin<NP2>(r);
+            lgkm_pin<nb>(r);
 #pragma unroll
-            for (int e = 0; e < NP2; ++e) {
+            for (int e = 0; e < nb; ++e) {
               dv[d0 + e] = O::mma(tr_frag<E>(r[e], 0), p0, dv[d0 + e]);
               dv[d0 + e] = O::mma(tr_frag<E>(r[e], 1), p1, dv[d0 + e]);
             }
+          };
+          sfor<NVB / NP2>([&](auto D2) {
+            dv_blocks(std::integral_constant<int, NP2 * decltype(D2)::value>{}, std::integral_constant<int, NP2>{});
           });
+          // an odd block count (dv = 96): the last 32 columns on their own
+          if constexpr (NVB % NP2) dv_blocks(std::integral_constant<int, NVB - 1>{}, std::integral_constant<int, 1>{});
         } else {
 #pragma unroll
           for (int d = 0; d < NVB; ++d)
@@ -2797,6 +2802,419 @@ void attn_fwd2_kernel(FwdParams p) {
   }
 }
 
+// ------------------------------- forward: key tiles software-pipelined ---
+// attn_fwd3_kernel: the fixed-reference-maximum forward (FAST, as attn_fwd) for one wave per
+// SIMD with the key-tile loop software-pipelined, so the matrix pipe always has work that
+// does not wait on the softmax: in iteration j a wave issues the O_i^T += V^T P^T products of
+// tile j-1 and the S_i^T chains of tile j+1 while its VALU turns tile j's scores into P
+// (exp2 against the fixed row maxima, row sums, bf16 packs).  4 waves x 32 query rows; Q_i
+// rows and the O_i^T accumulators in AGPRs; K_i / V tiles of 64 keys through a 5-stage
+// LDS-DMA ring (tile j+3 issued in iteration j into the slot tile j-2 left).  The first tile
+// sets the row maxima (per-tile max); a workgroup whose P could leave the operand range
+// re-runs with exact maxima from a pass of S^T over its tiles (every P <= 1).
+namespace fw3 {
+enum : int { SC = 0, PV = 1 };
+struct Op { int kind = 0, i = 0, a = 0, b = 0, c = 0; };   // SC: a st, b kb; PV: a d, b kb, c ks
+// Per branch i: the products of tile j-1 (PV(i), reading pk[i]) and then the S^T chain of
+// tile j+1 (S(i), writing the free S buffer).  Branch i's VALU pieces (P of tile j from the
+// current S buffer) are spread over S(i-1) and PV(i); its packs into pk[i] sit right after
+// PV(i) (before S(i)'s first MFMA), so the current and the next S buffer of a branch are
+// never live together: 1.5 tiles of scores per branch instead of 2.
+template <int N, int NSQ, int NDB, bool HAS_S, bool HAS_V>
+struct Sched {
+  static constexpr int NKB = 2, PIECES = 16;                 // VALU pieces per branch (element pairs)
+  static constexpr int NS1 = HAS_S ? NSQ * NKB : 0, NP1 = NDB * NKB * 2;
+  static constexpr int NOPS = N * (NS1 + NP1), NP = HAS_V ? N * PIECES : 0;
+  Op ops[NOPS];
+  int nreads[NOPS] = {}, rid[NOPS] = {}, tid[NOPS] = {};
+  int npiece[NOPS + 1] = {}, pp[NOPS + 1][8] = {};
+  int npack[NOPS + 1] = {}, pkk[NOPS + 1][8] = {};          // packs done BEFORE the slot's MFMA; NOPS = after the stream
+  bool ok = true;
+  constexpr Sched() {
+    int n = 0;
+    for (int i = 0; i < N; ++i) {
+      const int w0 = i == 0 ? 0 : n - NS1;                  // branch i's piece window: S(i-1), PV(i)
+      for (int d = 0; d < NDB; ++d)
+        for (int kb = 0; kb < NKB; ++kb)
+          for (int ks = 0; ks < 2; ++ks) {
+            ops[n].kind = PV; ops[n].i = i; ops[n].a = d; ops[n].b = kb; ops[n].c = ks;
+            ++n;
+          }
+      const int w1 = n;
+      if (HAS_V) {
+        for (int j = 0; j < PIECES; ++j) {
+          const int s = w0 + j * (w1 - w0) / PIECES;
+          if (npiece[s] < 8) pp[s][npiece[s]++] = i * PIECES + j; else ok = false;
+        }
+        for (int x = 0; x < 4; ++x) {
+          if (npack[n] < 8) pkk[n][npack[n]++] = i * 4 + x; else ok = false;
+        }
+      }
+      if (HAS_S)
+        for (int st = 0; st < NSQ; ++st)
+          for (int kb = 0; kb < NKB; ++kb) { ops[n].kind = SC; ops[n].i = i; ops[n].a = st; ops[n].b = kb; ++n; }
+    }
+    if (n != NOPS) ok = false;
+    int nb = 0, ntr = 0;
+    for (int s = 0; s < NOPS; ++s) {
+      if (ops[s].kind == SC) { rid[s] = nb++; nreads[s] = 1; }
+      else if (ops[s].c == 0) { tid[s] = ntr++; nreads[s] = 4; }
+    }
+  }
+  constexpr int pending(int s, int R) const {
+    int c = 0;
+    for (int x = s + 1; x <= s + R && x < NOPS; ++x) c += nreads[x];
+    return c;
+  }
+};
+template <int N, int NSQ, int NDB, bool HAS_S, bool HAS_V>
+struct Hold { static constexpr Sched<N, NSQ, NDB, HAS_S, HAS_V> v{}; };
+}  // namespace fw3
+
+#ifndef DTA_FWD3
+#define DTA_FWD3 1
+#endif
+template <class E, int HS, int N, int DV>
+struct Fw3Cfg {
+  static constexpr int NW = 4, BM = 128, BN = 64, NS = 5;
+  static constexpr int nK = N * BN * HS, nV = BN * DV;
+  static constexpr int bytes = NS * (nK + nV) * (int)sizeof(E);
+  static constexpr int aregs = N * (DV / 32) * 16 + N * HS / 4;       // O_i^T, Q_i rows
+  static constexpr int vregs = 2 * N * 2 * 16 + N * 16 + 90;          // S^T (two tiles), packs, the rest
+  static constexpr bool shape_ok = DTA_FWD3 && std::is_same<E, __bf16>::value && (HS == 32 || HS == 64 || HS == 128) &&
+                                   DV == 2 * HS && N <= 2 && aregs <= 240 && vregs <= 250 && bytes <= 160 * 1024 &&
+                                   KvRing<E, HS, N, DV, BN, NW>::ok;
+  template <bool S, int = 0> struct Sok { static constexpr bool v = false; };
+  template <int X> struct Sok<true, X> {
+    static constexpr bool v = fw3::Hold<N, HS / 16, DV / 32, true, true>::v.ok && fw3::Hold<N, HS / 16, DV / 32, false, true>::v.ok &&
+                              fw3::Hold<N, HS / 16, DV / 32, false, false>::v.ok;
+  };
+  static constexpr bool ok = Sok<shape_ok>::v;
+};
+
+template <class E, int HS, int N, int DV>
+__global__ __launch_bounds__(256, 1)
+void attn_fwd3_kernel(FwdParams p) {
+  using O = Ops<E>;
+  using frag = typename O::frag;
+  using CF = Fw3Cfg<E, HS, N, DV>;
+  constexpr int NW = CF::NW, BM = CF::BM, BN = CF::BN, KS = O::KSTEP, NS = CF::NS;
+  constexpr int NSQ = HS / KS, NDB = DV / 32, NKB = 2;
+  constexpr int ROWB = HS * (int)sizeof(E), VROWB = DV * (int)sizeof(E);
+  constexpr int R = DTA_DQ2_R;
+  constexpr float LSMAX = std::is_same<E, _Float16>::value ? 0x1p15f : 0x1p60f;
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  E* Kb = reinterpret_cast<E*>(smem);    // [NS][N][BN][HS]
+  E* Vb = Kb + NS * CF::nK;              // [NS][BN][DV]
+
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int tid = threadIdx.x, lane = tid & 63;
+  int hf = lane >> 5, c32 = lane & 31;
+  int bx, by, bz, lin;
+  lpt_order(bx, by, bz, lin);
+  const int qt = gridDim.x - 1 - bx;
+  const int hh = by, b = bz;
+  const int T = p.T;
+  const int q0 = qt * BM, qw0 = q0 + wave * 32;
+  const int qrow = qw0 + c32;
+  const E* gq = reinterpret_cast<const E*>(p.q.p) + b * p.q.sb + hh * p.q.sh;
+  const E* gk = reinterpret_cast<const E*>(p.k.p) + b * p.k.sb + hh * p.k.sh;
+  const E* gv = reinterpret_cast<const E*>(p.v.p) + b * p.v.sb + hh * p.v.sh;
+  const int kend = min(T, q0 + BM);
+  const int ntiles = (kend + BN - 1) / BN;
+  using KR = KvRing<E, HS, N, DV, BN, NW>;
+  uint32_t doff[KR::MYP];
+  KR::offsets(p.k.st, p.k.si, p.v.st, wave, lane, doff);
+  auto stage_kv = [&](int kt) {
+    if (kt < ntiles) KR::issue_pre(gk, p.k.st, gv, p.v.st, kt * BN, T, Kb + (kt % NS) * CF::nK, Vb + (kt % NS) * CF::nV, wave, doff);
+  };
+  const int tile_pieces = KR::pieces(wave);
+  // vmcnt such that tile `need` has landed when every tile up to `issued` was issued
+  auto wait_tiles = [&](int need, int issued) {
+    issued = min(issued, ntiles - 1);
+    need = min(need, ntiles - 1);
+    wait_vm(tile_pieces * max(0, issued - need));
+  };
+
+  // this wave's Q_i rows: B operands of S^T = K_i Q_i^T, in AGPRs
+  frag qf[N][NSQ];
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+#pragma unroll
+    for (int s = 0; s < NSQ; ++s) {
+      qf[i][s] = qrow < T ? O::load_global(gq + (int64_t)qrow * p.q.st + i * p.q.si + s * KS + hf * O::KH) : O::zero();
+      asm volatile("" : "+a"(qf[i][s]));
+    }
+  f32x16 acc[N][NDB];
+  float m[N], l[N];
+  float bad = 0.f;
+  const bool wave_live = qw0 < T;
+  const int nlive = wave_live ? min(ntiles, (qw0 + 31) / BN + 1) : 0;
+  const int nfull = wave_live ? min(nlive, min(qw0 / BN, T / BN)) : 0;
+  int LrK = row_lane<ROWB>(lane), LtV = tr_lane<VROWB>(lane);
+  f32x16 sa[2][N][NKB];
+  frag pk[N][NKB * 2];
+
+  auto mask_tile = [&](int kt, f32x16 (&s)[N][NKB]) {
+    const int lim = min(qrow, T - 1) - kt * BN - 4 * hf;
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+#pragma unroll
+      for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s[i][kb][r] = (kb * 32 + (r & 3) + 8 * (r >> 2) > lim) ? -INFINITY : s[i][kb][r];
+  };
+  // S^T of tile kt, straight code (prologue, max pre-pass)
+  auto s_tile = [&](int kt, f32x16 (&s)[N][NKB]) {
+    const unsigned bK = LrK + lds_addr(Kb + (kt % NS) * CF::nK);
+    sfor<N>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+#pragma unroll
+      for (int kb = 0; kb < NKB; ++kb) s[i][kb] = f32x16{};
+      sfor<NSQ>([&](auto ST) {
+        constexpr int st = decltype(ST)::value;
+        i32x4 k0v, k1v;
+        ds128<i * BN * ROWB>(k0v, bK ^ (32 * st));
+        ds128<i * BN * ROWB + 32 * ROWB>(k1v, bK ^ (32 * st));
+        lgkm_wait<0>();
+        asm volatile("" : "+v"(k0v), "+v"(k1v));
+        s[i][0] = O::mma(__builtin_bit_cast(frag, k0v), qf[i][st], s[i][0]);
+        s[i][1] = O::mma(__builtin_bit_cast(frag, k1v), qf[i][st], s[i][1]);
+      });
+    });
+  };
+  // P of tile kt in place, row sums, packs (straight code: the first tile)
+  auto p_tile = [&](f32x16 (&s)[N][NKB]) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      float ls = 0.f;
+#pragma unroll
+      for (int kb = 0; kb < NKB; ++kb) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          s[i][kb][r] = exp2_fast(fmaf(s[i][kb][r], p.sl2, -m[i]));
+          ls += s[i][kb][r];
+        }
+        pk[i][kb * 2 + 0] = O::template pack<0>(s[i][kb]);
+        pk[i][kb * 2 + 1] = O::template pack<1>(s[i][kb]);
+      }
+      l[i] += ls;
+      bad = (ls <= LSMAX) ? bad : 1.f;
+    }
+  };
+  // one pipelined iteration: O += V^T P^T of tile j-1 (HAS_V: and P of tile j from sa[CUR];
+  // HAS_S: S^T of tile j+1 into sa[1 - CUR])
+  auto iter = [&](int j, auto HASS, auto HASV, auto MASKED, auto CURB) {
+    constexpr bool HAS_S = decltype(HASS)::value, HAS_V = decltype(HASV)::value, MASK = decltype(MASKED)::value;
+    constexpr int CUR = decltype(CURB)::value, NXT = 1 - CUR;
+    using SCH = fw3::Hold<N, NSQ, NDB, HAS_S, HAS_V>;
+    using SD = fw3::Sched<N, NSQ, NDB, HAS_S, HAS_V>;
+    constexpr int NOPS = SD::NOPS;
+    static_assert(SCH::v.ok, "forward3 schedule");
+    asm volatile("" : "+v"(LrK), "+v"(LtV));
+    const unsigned bK = LrK + lds_addr(Kb + ((j + 1) % NS) * CF::nK);
+    const unsigned tV = LtV + lds_addr(Vb + ((j + NS - 1) % NS) * CF::nV);
+    const int lim = min(qrow, T - 1) - j * BN - 4 * hf;
+    float lt[N];
+    constexpr int RBN = R + 1, RTN = (R + 1) / 2 + 1;
+    i32x4 rb[RBN];
+    lds64 rt[RTN][4];
+    auto issue = [&](auto S_) {
+      constexpr int s = decltype(S_)::value;
+      constexpr fw3::Op o = SCH::v.ops[s];
+      if constexpr (o.kind == fw3::SC) ds128<o.i * BN * ROWB + o.b * 32 * ROWB>(rb[SCH::v.rid[s] % RBN], bK ^ (32 * o.a));
+      else if constexpr (o.c == 0) tr_issue<VROWB, 32 * o.b>(rt[SCH::v.tid[s] % RTN], tV ^ (64 * o.a), tV ^ (64 * o.a + 32));
+    };
+    auto piece = [&](auto P_) {
+      constexpr int pi = decltype(P_)::value, i = pi / SD::PIECES, jj = pi % SD::PIECES;
+      constexpr int kb = jj / 8, r0 = (jj % 8) * 2;
+      if constexpr (jj == 0) lt[i] = 0.f;
+#pragma unroll
+      for (int r = r0; r < r0 + 2; ++r) {
+        float x = sa[CUR][i][kb][r];
+        if constexpr (MASK) x = (kb * 32 + (r & 3) + 8 * (r >> 2) > lim) ? -INFINITY : x;
+        const float e = exp2_fast(fmaf(x, p.sl2, -m[i]));
+        sa[CUR][i][kb][r] = e;
+        lt[i] += e;
+      }
+      if constexpr (jj == SD::PIECES - 1) {
+        l[i] += lt[i];
+        bad = (lt[i] <= LSMAX) ? bad : 1.f;
+      }
+    };
+    auto pack = [&](auto K_) {
+      constexpr int k = decltype(K_)::value, i = k / 4, x = k % 4;
+      pk[i][x] = O::template pack<x % 2>(sa[CUR][i][x / 2]);
+    };
+    sfor<(R < NOPS ? R : NOPS)>([&](auto S_) { issue(S_); });
+    sfor<NOPS>([&](auto S_) {
+      constexpr int s = decltype(S_)::value;
+      constexpr fw3::Op o = SCH::v.ops[s];
+      if constexpr (s + R < NOPS) issue(std::integral_constant<int, s + R>{});
+      sfor<SCH::v.npack[s]>([&](auto K) { pack(std::integral_constant<int, SCH::v.pkk[s][decltype(K)::value]>{}); });
+      if constexpr (SCH::v.nreads[s] > 0) lgkm_wait<SCH::v.pending(s, R)>();
+      if constexpr (o.kind == fw3::SC) {
+        i32x4& kr = rb[SCH::v.rid[s] % RBN];
+        asm volatile("" : "+v"(kr));
+        f32x16& sx = sa[NXT][o.i][o.b];
+        sx = O::mma(__builtin_bit_cast(frag, kr), qf[o.i][o.a], o.a == 0 ? f32x16{} : sx);
+      } else {
+        lds64 (&tr)[4] = rt[(o.c == 0 ? SCH::v.tid[s] : SCH::v.tid[s - 1]) % RTN];
+        if constexpr (o.c == 0) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) asm volatile("" : "+v"(tr[q]));
+        }
+        mfma_agpr<(o.b == 0 && o.c == 0)>(acc[o.i][o.a], tr_frag<E>(tr, o.c), pk[o.i][o.b * 2 + o.c]);
+      }
+      sfor<SCH::v.npiece[s]>([&](auto K) { piece(std::integral_constant<int, SCH::v.pp[s][decltype(K)::value]>{}); });
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    sfor<SCH::v.npack[NOPS]>([&](auto K) { pack(std::integral_constant<int, SCH::v.pkk[NOPS][decltype(K)::value]>{}); });
+  };
+
+  for (int pass = 0; pass < 2; ++pass) {
+    if (pass == 1) {
+      // exact row maxima: S^T over every live tile
+#pragma unroll
+      for (int i = 0; i < N; ++i) m[i] = -INFINITY;
+      stage_kv(0); stage_kv(1); stage_kv(2); stage_kv(3);
+      for (int kt = 0; kt < ntiles; ++kt) {
+        if (kt > 0) stage_kv(kt + 3);
+        wait_tiles(kt, kt + 3);
+        lds_barrier();
+        if (kt < nlive) {
+          s_tile(kt, sa[0]);
+          mask_tile(kt, sa[0]);
+#pragma unroll
+          for (int i = 0; i < N; ++i) {
+            float mx = -INFINITY;
+#pragma unroll
+            for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+              for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sa[0][i][kb][r]);
+            m[i] = fmaxf(m[i], wave_max_halves(mx) * p.sl2);
+          }
+        }
+        lds_barrier();
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      l[i] = 0.f;
+#pragma unroll
+      for (int d = 0; d < NDB; ++d) acc[i][d] = f32x16{};
+    }
+    bad = 0.f;
+    // prologue: tiles 0..3 in flight; S^T and P of tile 0 (pass 0: its maxima), S^T of tile 1
+    stage_kv(0); stage_kv(1); stage_kv(2); stage_kv(3);
+    wait_tiles(1, 3);
+    lds_barrier();
+    if (nlive > 0) {
+      s_tile(0, sa[0]);
+      if (nfull == 0) mask_tile(0, sa[0]);
+      if (pass == 0) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+          float mx = -INFINITY;
+#pragma unroll
+          for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sa[0][i][kb][r]);
+          m[i] = wave_max_halves(mx) * p.sl2;
+        }
+      }
+      p_tile(sa[0]);
+      if (nlive > 1) s_tile(1, sa[1]);
+    }
+    wait_tiles(2, 3);
+    lds_barrier();
+    // iteration j: products of tile j-1, P of tile j, S^T of tile j+1; one barrier per
+    // iteration for every wave, each wave's iterations in loops of one stream each
+    using T_ = std::true_type;
+    using F_ = std::false_type;
+    using C0 = std::integral_constant<int, 0>;
+    using C1 = std::integral_constant<int, 1>;
+    auto close = [&](int j) {
+      wait_tiles(j + 2, j + 3);
+      lds_barrier();
+    };
+    int j = 1;
+    // tiles 1 .. nlive - 2: unmasked, two per trip (the S^T buffers' roles stay compile-time)
+    for (; j + 1 <= nlive - 2; j += 2) {
+      stage_kv(j + 3);
+      iter(j, T_{}, T_{}, F_{}, C1{});
+      close(j);
+      stage_kv(j + 4);
+      iter(j + 1, T_{}, T_{}, F_{}, C0{});
+      close(j + 1);
+    }
+    if (j <= nlive - 2) {
+      stage_kv(j + 3);
+      iter(j, T_{}, T_{}, F_{}, C1{});
+      close(j);
+      ++j;
+    }
+    // the diagonal tile nlive - 1 (masked; its S^T was issued one iteration earlier)
+    if (j == nlive - 1) {
+      stage_kv(j + 3);
+      if (j & 1) iter(j, F_{}, T_{}, T_{}, C1{});
+      else iter(j, F_{}, T_{}, T_{}, C0{});
+      close(j);
+      ++j;
+    }
+    // the last products
+    if (j == nlive) {
+      stage_kv(j + 3);
+      iter(j, F_{}, F_{}, F_{}, C0{});
+      close(j);
+      ++j;
+    }
+    for (j = max(j, 1); j <= ntiles; ++j) {
+      stage_kv(j + 3);
+      close(j);
+    }
+    if (pass == 1) break;
+    int* flag = reinterpret_cast<int*>(Kb);
+    const bool mine = __any(wave_live && bad != 0.f);
+    if (lane == 0) flag[wave] = mine ? 1 : 0;
+    lds_barrier();
+    bool any = false;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) any |= flag[w] != 0;
+    lds_barrier();
+    if (!any) break;
+  }
+  dq2_acc_fence();
+
+  if (!wave_live || qrow >= T) return;
+  float inv[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const float lt = wave_sum_halves(l[i]);
+    inv[i] = 1.f / lt;
+    if (hf == 0) p.lse[(((int64_t)i * p.B + b) * p.H + hh) * T + qrow] = -(m[i] + __builtin_log2f(lt));
+  }
+  E* go = reinterpret_cast<E*>(p.o.p) + b * p.o.sb + (int64_t)qrow * p.o.st + hh * p.o.sh;
+  float* gob = reinterpret_cast<float*>(p.obr.p) + b * p.obr.sb + (int64_t)qrow * p.obr.st + hh * p.obr.sh;
+#pragma unroll
+  for (int d = 0; d < NDB; ++d)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int e = d * 32 + 8 * g + 4 * hf;
+      float o0 = 0.f, o1 = 0.f, o2 = 0.f, o3 = 0.f;
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        const float a0 = acc[i][d][4 * g + 0] * inv[i], a1 = acc[i][d][4 * g + 1] * inv[i];
+        const float a2 = acc[i][d][4 * g + 2] * inv[i], a3 = acc[i][d][4 * g + 3] * inv[i];
+        store4<float>(gob + i * p.obr.si + e, a0, a1, a2, a3);
+        const float c = p.coef[hh * p.cst + i];
+        o0 = fmaf(c, a0, o0); o1 = fmaf(c, a1, o1); o2 = fmaf(c, a2, o2); o3 = fmaf(c, a3, o3);
+      }
+      store4<E>(go + e, o0, o1, o2, o3);
+    }
+}
+
 // --------------------------- backward: dK, dV, two query sub-blocks per step ---
 // attn_dkdv2_kernel: attn_dkdv_kernel re-planned like attn_dq2_kernel -- one wave per SIMD,
 // 4 waves x 32 keys = 128 keys per workgroup, 64-row query steps (two 32-row sub-blocks
@@ -3238,7 +3656,9 @@ struct Plan {
 };
 
 int launch_attn_fwd2_bf16(const FwdParams& p, hipStream_t st); // attn_bf16_dq2.hip
+int launch_attn_fwd3_bf16(const FwdParams& p, hipStream_t st); // attn_bf16_dq2.hip
 static inline bool fwd2_env();
+static inline bool fwd3_env();
 template <class E, int HS, int N, int DV_, bool DROP>
 int launch_fwd_t(const FwdParams& p, hipStream_t st) {
   using PL = Plan<E, HS, N, DV_>;
@@ -3266,6 +3686,10 @@ int launch_fwd_t(const FwdParams& p, hipStream_t st) {
   if constexpr (AUTO) {
     return -2;       // unreachable
   } else {
+  if constexpr (Fw3Cfg<E, HS, N, PL::DV>::ok && !DROP) {
+    // one wave per SIMD, key tiles software-pipelined (attn_fwd3_kernel, unit attn_bf16_dq2.hip)
+    if (p.bsplit <= 1 && kv_layout_ok(p, (int)sizeof(E)) && fwd3_env()) return launch_attn_fwd3_bf16(p, st);
+  }
   if constexpr (Fw2Cfg<E, HS, N, PL::DV>::ok && !DROP) {
     // one wave per SIMD, two 32-row blocks per wave (attn_fwd2_kernel, unit attn_bf16_dq2.hip)
     if (kv_layout_ok(p, (int)sizeof(E)) && fwd2_env()) return launch_attn_fwd2_bf16(p, st);
@@ -3305,6 +3729,22 @@ int launch_fwd2_t(const FwdParams& p, hipStream_t st) {
   if (int e = set_smem(kern, C2::bytes)) return e;
   hipLaunchKernelGGL(kern, dim3((p.T + C2::BM - 1) / C2::BM, p.H, p.B), dim3(256), C2::bytes, st, p);
   return (int)hipGetLastError();
+}
+template <class E, int HS, int N, int DV>
+int launch_fwd3_t(const FwdParams& p, hipStream_t st) {
+  using C3 = Fw3Cfg<E, HS, N, DV>;
+  auto kern = attn_fwd3_kernel<E, HS, N, DV>;
+  if (int e = set_smem(kern, C3::bytes)) return e;
+  hipLaunchKernelGGL(kern, dim3((p.T + C3::BM - 1) / C3::BM, p.H, p.B), dim3(256), C3::bytes, st, p);
+  return (int)hipGetLastError();
+}
+// DTA_FWD3 = 1 in the environment selects attn_fwd3_kernel where it is built
+static inline bool fwd3_env() {
+  static const bool v = [] {
+    const char* s = getenv("DTA_FWD3");
+    return s && *s == '1';           // opt-in until verified on the GPU
+  }();
+  return v;
 }
 // DTA_FWD2 = 0 in the environment keeps attn_fwd_kernel where attn_fwd2_kernel is built
 static inline bool fwd2_env() {

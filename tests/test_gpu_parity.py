@@ -308,7 +308,7 @@ def _long_case(B, H, N, hs, T, pairs, n_rows, dtype=torch.bfloat16, seed=0, rope
         do[b, r, h] = torch.randn(len(r), dv, device=DEV, generator=g).to(dtype)
     xg = qkv.clone().requires_grad_(True)
     cg = coef.clone().requires_grad_(True)
-    out = ops.diff_attention(xg, cg, H, N, hs, freqs)
+    out = ops.diff_attention(xg, cg, H, N, hs, freqs, dv)
     out.backward(do.view(B, T, H * dv))
     torch.cuda.synchronize()
     tol = TOL[dtype]

@@ -116,7 +116,10 @@ def test_default_config_diff_transformer_bf16_autocast():
     # d(lambda) = 2.6e-4 against sum|terms| = 4.07, 1.6e4 : 1), so one bf16 rounding anywhere
     # upstream moves it by O(1).  Each head's lambda gradient is therefore held, head by
     # head, to 2x the error of the reference algorithm itself under the same bf16 autocast
-    # (the oracle model run on the GPU), at least 2e-2.  Every error and bar is logged.
+    # (the oracle model run on the GPU), at least 2e-2.  A non-lambda parameter is held to
+    # 2e-2, or -- where the reference algorithm itself under bf16 autocast misses 2e-2 on it
+    # (measured: block 1 head 1's query / key weights, 2.3e-2 .. 3.1e-2, from its bf16 score
+    # matrix) -- to that error: never worse than the reference.  Every error and bar is logged.
     sd32 = {k: v.detach().float().to(DEV).requires_grad_(True) for k, v in sd.items()}
     with torch.autocast("cuda", dtype=torch.bfloat16):
         _, l32 = _oracle_diff_transformer(sd32, idx.to(DEV), tgt.to(DEV), 4, 2, 512)
@@ -127,7 +130,7 @@ def test_default_config_diff_transformer_bf16_autocast():
             continue
         got, ref, r32 = p.grad.double().cpu(), sd[n].grad, sd32[n].grad.double().cpu()
         err, ref_err = rel_err(got, ref), rel_err(r32, ref)
-        bar = max(2e-2, 2.0 * ref_err) if ".lambda_" in n else 2e-2
+        bar = max(2e-2, 2.0 * ref_err) if ".lambda_" in n else max(2e-2, ref_err)
         log.append({"param": n, "err": err, "ref_alg_bf16_err": ref_err, "bar": bar})
         if not err < bar:
             bad.append((n, err, ref_err, bar))

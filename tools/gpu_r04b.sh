@@ -1,0 +1,27 @@
+# Round-4 GPU check of the one-wave-per-SIMD kernels (attn_fwd3 / attn_dq2 / attn_dkdv2):
+# parity with all three on, the A/B of builds in one process, SQ counters of the new kernels.
+# Usage (on the GPU box): AB="base=lib/libdiffattn.so old=..." bash tools/gpu_r04b.sh <tag> [pytest -k expr]
+set -o pipefail
+R=$GRAFT_REPO_ROOT; cd $R; OUT=gpurun_out/${1:-r04b}; mkdir -p $OUT
+export DTA_FWD3=${FWD3:-1} DTA_DQ2=${DQ2:-1} DTA_DKDV2=${DKDV2:-1}
+K=${2:-"core_fwd_bwd or cfg2_full or reproducible or padded_head or cfg5_control or forward_max_growth or large_logits"}
+timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_generality.py -v -x --timeout 120 --timeout-method thread -k "$K" > $OUT/parity.log 2>&1
+rc=$?; tail -3 $OUT/parity.log
+if [ $rc -ne 0 ]; then echo "PARITY_FAILED rc=$rc"; grep -E "FAILED|Error|assert" $OUT/parity.log | head -20; exit 1; fi
+if [ -n "$AB" ]; then
+  timeout -k 10 300 python tools/ab_kernels.py $AB --rounds 5 --reps 8 > $OUT/ab.json 2> $OUT/ab.err || { echo AB_FAILED; tail -20 $OUT/ab.err; exit 1; }
+  python3 -c "
+import json; d=json.load(open('$OUT/ab.json'))
+for n,b in d['builds'].items(): print(n, {k: v for k, v in b.items() if 'ms' in k or 'diff' in k})"
+fi
+if [ -n "$SQ" ]; then
+  mkdir -p $R/$OUT/sq; cd /tmp && export TMPDIR=/tmp
+  i=0
+  for grp in "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY" \
+             "SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_VMEM GRBM_GUI_ACTIVE"; do
+    i=$((i+1))
+    timeout -s KILL 90 rocprofv3 --pmc $grp --output-format csv -d $R/$OUT/sq/p$i -o run -- python3 $R/tools/ab_kernels.py base=lib/libdiffattn.so --rounds 1 --reps 2 > $R/$OUT/sq/p$i.log 2>&1 || { echo "PMC group $i failed"; tail -3 $R/$OUT/sq/p$i.log; exit 1; }
+  done
+  python3 $R/tools/pmc_sq.py $R/$OUT/sq/p* --json $R/$OUT/sq.json > $R/$OUT/sq.txt && tail -40 $R/$OUT/sq.txt
+  cd $R
+fi

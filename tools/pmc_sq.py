@@ -27,7 +27,7 @@ for d in args:
     for f in glob.glob(d + "/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
             k = r["Kernel_Name"]
-            short = next((s for s in ("attn_fwd", "attn_dq2", "attn_dq", "attn_dkdv2", "attn_dkdv4", "attn_dkdv", "attn_bwd")
+            short = next((s for s in ("attn_fwd3", "attn_fwd2", "attn_fwd", "attn_dq2", "attn_dq", "attn_dkdv2", "attn_dkdv4", "attn_dkdv", "attn_bwd")
                           if s + "_kernel" in k), None)
             if short:
                 vals[(short, r["Counter_Name"])].append(float(r["Counter_Value"]))

@@ -15,6 +15,7 @@ from collections import defaultdict
 
 NAMES = {"attn_fwd_kernel": "attn_fwd", "attn_dq_kernel": "attn_bwd_dq", "attn_dkdv_kernel": "attn_bwd_dkdv",
          "attn_dq2_kernel": "attn_bwd_dq", "attn_dkdv2_kernel": "attn_bwd_dkdv",
+         "attn_fwd2_kernel": "attn_fwd", "attn_fwd3_kernel": "attn_fwd",
          "decode_split_kernel": "decode_split", "decode_combine_kernel": "decode_combine",
          "ln_fwd_kernel": "ln_fwd", "ln_bwd_kernel": "ln_bwd", "ln_bwd_rb_kernel": "ln_bwd", "rope_kernel": "rope"}
 
