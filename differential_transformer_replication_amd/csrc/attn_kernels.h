@@ -498,6 +498,21 @@ struct KvRing {
       else off[u] = j < PK ? offk(kst, ksi, j, lane) : (j < NPC ? offv(vst, j, lane) : 0u);
     });
   }
+  // piece u of this wave's share of one tile (a scheduled stream spreads them over its slots)
+  template <int u>
+  __device__ static void issue_one(const E* gk, int64_t kst, const E* gv, int64_t vst, int k0, int T, E* kdst,
+                                   E* vdst, int wave, uint32_t off) {
+    const int rows = max(0, T - k0);
+    const int j = u * NW + wave;
+    if constexpr ((u + 1) * NW <= PK) {
+      buf_lds16(gk + (int64_t)k0 * kst, (uint32_t)rows * (uint32_t)(kst * ES), reinterpret_cast<char*>(kdst) + j * 1024, off);
+    } else if constexpr (u * NW >= PK && (u + 1) * NW <= NPC) {
+      buf_lds16(gv + (int64_t)k0 * vst, (uint32_t)rows * (uint32_t)(vst * ES), reinterpret_cast<char*>(vdst) + (j - PK) * 1024, off);
+    } else {
+      if (j < PK) buf_lds16(gk + (int64_t)k0 * kst, (uint32_t)rows * (uint32_t)(kst * ES), reinterpret_cast<char*>(kdst) + j * 1024, off);
+      else if (j < NPC) buf_lds16(gv + (int64_t)k0 * vst, (uint32_t)rows * (uint32_t)(vst * ES), reinterpret_cast<char*>(vdst) + (j - PK) * 1024, off);
+    }
+  }
   __device__ static void issue_pre(const E* gk, int64_t kst, const E* gv, int64_t vst, int k0, int T, E* kdst,
                                    E* vdst, int wave, const uint32_t (&off)[MYP]) {
     const int rows = max(0, T - k0);
@@ -1502,6 +1517,14 @@ __device__ __forceinline__ void mfma_agpr(f32x16& acc, bf16x8 a, bf16x8 b) {
   else asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
 }
 __device__ __forceinline__ void dq2_acc_fence() { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory"); }
+// pin accumulators after a fence: their readers (v_accvgpr_read, allocator copies) then
+// depend on the pins, which volatile ordering keeps after the fence's wait states
+__device__ __forceinline__ void acc_pin(f32x16& a) { asm volatile("" : "+a"(a)); }
+template <class A, int M>
+__device__ __forceinline__ void acc_pin(A (&a)[M]) {
+#pragma unroll
+  for (int i = 0; i < M; ++i) acc_pin(a[i]);
+}
 
 namespace dq2 {
 enum : int { SS = 0, SC = 1, DS = 2, DC = 3, CC = 4 };
@@ -1749,7 +1772,7 @@ void attn_dq2_kernel(BwdParams p) {
   int LrV = row_lane<VROWB>(lane), LrK = row_lane<ROWB>(lane), LtK = tr_lane<ROWB>(lane);
 
   // one tile: the MFMA stream with the VALU pieces in its slots
-  auto body = [&](int kt, auto MASKED) {
+  auto body = [&](int kt, auto MASKED, int kt_dma) {
     constexpr bool MASK = decltype(MASKED)::value;
     asm volatile("" : "+v"(LrV), "+v"(LrK), "+v"(LtK));
     // the seed MFMAs are loop-invariant: keep them in the tile (an opaque "ones" operand),
@@ -1798,6 +1821,14 @@ void attn_dq2_kernel(BwdParams p) {
       constexpr int s = decltype(S_)::value;
       constexpr dq2::Op o = SCH::v.ops[s];
       if constexpr (s + R < NOPS) issue(std::integral_constant<int, s + R>{});
+      // this wave's LDS-DMA pieces of tile kt_dma, spread over the stream
+      sfor<KR::MYP>([&](auto U) {
+        constexpr int u = decltype(U)::value;
+        if constexpr (s == (u + 1) * NOPS / (KR::MYP + 1))
+          if (kt_dma < ntiles)
+            KR::template issue_one<u>(gk, p.k.st, gv, p.v.st, kt_dma * BN, T, Kb + (kt_dma % NS) * CF::nK,
+                                      Vb + (kt_dma % NS) * CF::nV, wave, doff[u]);
+      });
       if constexpr (SCH::v.nreads[s] > 0) lgkm_wait<SCH::v.pending(s, R)>();
       if constexpr (o.kind == dq2::SS) {
         sa[o.u % 2][o.b] = O::mma(one, f_lse[o.qb][o.i], f32x16{});
@@ -1825,8 +1856,8 @@ void attn_dq2_kernel(BwdParams p) {
     });
   };
   auto step = [&](int kt, auto MASKED, bool live) {
-    if (kt + NS - 1 < ntiles) stage_kv(kt + NS - 1, (kt + NS - 1) % NS);
-    if (live) body(kt, MASKED);
+    if (live) body(kt, MASKED, kt + NS - 1);
+    else if (kt + NS - 1 < ntiles) stage_kv(kt + NS - 1, (kt + NS - 1) % NS);
     wait_vm(tile_pieces * max(0, min(NS - 2, ntiles - 2 - kt)));
     lds_barrier();
   };
@@ -1839,6 +1870,7 @@ void attn_dq2_kernel(BwdParams p) {
   for (int kt = nfull; kt < nlive; ++kt) step(kt, std::true_type{}, true);
   for (int kt = nlive; kt < ntiles; ++kt) step(kt, std::false_type{}, false);
   dq2_acc_fence();
+  acc_pin(dq);
 
 #pragma unroll
   for (int qb = 0; qb < 2; ++qb) {
@@ -2766,6 +2798,7 @@ void attn_fwd2_kernel(FwdParams p) {
     if (!any) break;
   }
   dq2_acc_fence();
+  acc_pin(acc);
 
   if (!wave_live) return;
 #pragma unroll
@@ -2882,8 +2915,8 @@ struct Fw3Cfg {
   static constexpr int aregs = N * (DV / 32) * 16 + N * HS / 4;       // O_i^T, Q_i rows
   static constexpr int vregs = 2 * N * 2 * 16 + N * 16 + 90;          // S^T (two tiles), packs, the rest
   static constexpr bool shape_ok = DTA_FWD3 && std::is_same<E, __bf16>::value && (HS == 32 || HS == 64 || HS == 128) &&
-                                   DV == 2 * HS && N <= 2 && aregs <= 240 && vregs <= 250 && bytes <= 160 * 1024 &&
-                                   KvRing<E, HS, N, DV, BN, NW>::ok;
+                                   (DV == 2 * HS || (N == 1 && DV == HS)) && N <= 2 && aregs <= 240 && vregs <= 250 &&
+                                   bytes <= 160 * 1024 && KvRing<E, HS, N, DV, BN, NW>::ok;
   template <bool S, int = 0> struct Sok { static constexpr bool v = false; };
   template <int X> struct Sok<true, X> {
     static constexpr bool v = fw3::Hold<N, HS / 16, DV / 32, true, true>::v.ok && fw3::Hold<N, HS / 16, DV / 32, false, true>::v.ok &&
@@ -2914,12 +2947,15 @@ void attn_fwd3_kernel(FwdParams p) {
   int bx, by, bz, lin;
   lpt_order(bx, by, bz, lin);
   const int qt = gridDim.x - 1 - bx;
-  const int hh = by, b = bz;
+  // branch-split launch (N == 1 instantiation, p.bsplit branches per head, as attn_fwd):
+  // workgroup (head, branch br) writes O_br and LSE_br; a combine pass forms O
+  const int nsp = (N == 1 && p.bsplit > 1) ? p.bsplit : 1;
+  const int hh = by / nsp, br = by - hh * nsp, b = bz;
   const int T = p.T;
   const int q0 = qt * BM, qw0 = q0 + wave * 32;
   const int qrow = qw0 + c32;
-  const E* gq = reinterpret_cast<const E*>(p.q.p) + b * p.q.sb + hh * p.q.sh;
-  const E* gk = reinterpret_cast<const E*>(p.k.p) + b * p.k.sb + hh * p.k.sh;
+  const E* gq = reinterpret_cast<const E*>(p.q.p) + b * p.q.sb + hh * p.q.sh + br * p.q.si;
+  const E* gk = reinterpret_cast<const E*>(p.k.p) + b * p.k.sb + hh * p.k.sh + br * p.k.si;
   const E* gv = reinterpret_cast<const E*>(p.v.p) + b * p.v.sb + hh * p.v.sh;
   const int kend = min(T, q0 + BM);
   const int ntiles = (kend + BN - 1) / BN;
@@ -3005,7 +3041,7 @@ void attn_fwd3_kernel(FwdParams p) {
   };
   // one pipelined iteration: O += V^T P^T of tile j-1 (HAS_V: and P of tile j from sa[CUR];
   // HAS_S: S^T of tile j+1 into sa[1 - CUR])
-  auto iter = [&](int j, auto HASS, auto HASV, auto MASKED, auto CURB) {
+  auto iter = [&](int j, auto HASS, auto HASV, auto MASKED, auto CURB, int kt_dma) {
     constexpr bool HAS_S = decltype(HASS)::value, HAS_V = decltype(HASV)::value, MASK = decltype(MASKED)::value;
     constexpr int CUR = decltype(CURB)::value, NXT = 1 - CUR;
     using SCH = fw3::Hold<N, NSQ, NDB, HAS_S, HAS_V>;
@@ -3030,10 +3066,13 @@ void attn_fwd3_kernel(FwdParams p) {
       constexpr int pi = decltype(P_)::value, i = pi / SD::PIECES, jj = pi % SD::PIECES;
       constexpr int kb = jj / 8, r0 = (jj % 8) * 2;
       if constexpr (jj == 0) lt[i] = 0.f;
+      // the compares stay in their piece (hoisted, the 32 lane masks of a tile fill the SGPRs)
+      int lm = lim;
+      if constexpr (MASK) asm volatile("" : "+v"(lm));
 #pragma unroll
       for (int r = r0; r < r0 + 2; ++r) {
         float x = sa[CUR][i][kb][r];
-        if constexpr (MASK) x = (kb * 32 + (r & 3) + 8 * (r >> 2) > lim) ? -INFINITY : x;
+        if constexpr (MASK) x = (kb * 32 + (r & 3) + 8 * (r >> 2) > lm) ? -INFINITY : x;
         const float e = exp2_fast(fmaf(x, p.sl2, -m[i]));
         sa[CUR][i][kb][r] = e;
         lt[i] += e;
@@ -3052,6 +3091,15 @@ void attn_fwd3_kernel(FwdParams p) {
       constexpr int s = decltype(S_)::value;
       constexpr fw3::Op o = SCH::v.ops[s];
       if constexpr (s + R < NOPS) issue(std::integral_constant<int, s + R>{});
+      // this wave's LDS-DMA pieces of tile kt_dma, spread over the stream (issued in one
+      // burst they held the MFMAs for ~60+ cycles each)
+      sfor<KR::MYP>([&](auto U) {
+        constexpr int u = decltype(U)::value;
+        if constexpr (s == (u + 1) * NOPS / (KR::MYP + 1))
+          if (kt_dma < ntiles)
+            KR::template issue_one<u>(gk, p.k.st, gv, p.v.st, kt_dma * BN, T, Kb + (kt_dma % NS) * CF::nK,
+                                      Vb + (kt_dma % NS) * CF::nV, wave, doff[u]);
+      });
       sfor<SCH::v.npack[s]>([&](auto K) { pack(std::integral_constant<int, SCH::v.pkk[s][decltype(K)::value]>{}); });
       if constexpr (SCH::v.nreads[s] > 0) lgkm_wait<SCH::v.pending(s, R)>();
       if constexpr (o.kind == fw3::SC) {
@@ -3071,6 +3119,11 @@ void attn_fwd3_kernel(FwdParams p) {
       __builtin_amdgcn_sched_barrier(0);
     });
     sfor<SCH::v.npack[NOPS]>([&](auto K) { pack(std::integral_constant<int, SCH::v.pkk[NOPS][decltype(K)::value]>{}); });
+    // the O_i^T accumulators are written by asm MFMAs whose latency the compiler does not
+    // see: before any register-allocator copy between AGPRs at the next control-flow
+    // merge, the last MFMA must have landed
+    dq2_acc_fence();
+    acc_pin(acc);
   };
 
   for (int pass = 0; pass < 2; ++pass) {
@@ -3142,31 +3195,33 @@ void attn_fwd3_kernel(FwdParams p) {
     int j = 1;
     // tiles 1 .. nlive - 2: unmasked, two per trip (the S^T buffers' roles stay compile-time)
     for (; j + 1 <= nlive - 2; j += 2) {
-      stage_kv(j + 3);
-      iter(j, T_{}, T_{}, F_{}, C1{});
+      iter(j, T_{}, T_{}, F_{}, C1{}, j + 3);
       close(j);
-      stage_kv(j + 4);
-      iter(j + 1, T_{}, T_{}, F_{}, C0{});
+      iter(j + 1, T_{}, T_{}, F_{}, C0{}, j + 4);
       close(j + 1);
     }
     if (j <= nlive - 2) {
-      stage_kv(j + 3);
-      iter(j, T_{}, T_{}, F_{}, C1{});
+      iter(j, T_{}, T_{}, F_{}, C1{}, j + 3);
       close(j);
       ++j;
     }
     // the diagonal tile nlive - 1 (masked; its S^T was issued one iteration earlier)
     if (j == nlive - 1) {
-      stage_kv(j + 3);
-      if (j & 1) iter(j, F_{}, T_{}, T_{}, C1{});
-      else iter(j, F_{}, T_{}, T_{}, C0{});
+      // one instance of this stream: its scores moved into the first buffer (two instances
+      // merging into the last products made the allocator copy O_i^T between AGPRs)
+      if (j & 1) {
+#pragma unroll
+        for (int i = 0; i < N; ++i)
+#pragma unroll
+          for (int kb = 0; kb < NKB; ++kb) sa[0][i][kb] = sa[1][i][kb];
+      }
+      iter(j, F_{}, T_{}, T_{}, C0{}, j + 3);
       close(j);
       ++j;
     }
     // the last products
     if (j == nlive) {
-      stage_kv(j + 3);
-      iter(j, F_{}, F_{}, F_{}, C0{});
+      iter(j, F_{}, F_{}, F_{}, C0{}, j + 3);
       close(j);
       ++j;
     }
@@ -3186,6 +3241,7 @@ void attn_fwd3_kernel(FwdParams p) {
     if (!any) break;
   }
   dq2_acc_fence();
+  acc_pin(acc);
 
   if (!wave_live || qrow >= T) return;
   float inv[N];
@@ -3193,10 +3249,10 @@ void attn_fwd3_kernel(FwdParams p) {
   for (int i = 0; i < N; ++i) {
     const float lt = wave_sum_halves(l[i]);
     inv[i] = 1.f / lt;
-    if (hf == 0) p.lse[(((int64_t)i * p.B + b) * p.H + hh) * T + qrow] = -(m[i] + __builtin_log2f(lt));
+    if (hf == 0) p.lse[(((int64_t)(br + i) * p.B + b) * p.H + hh) * T + qrow] = -(m[i] + __builtin_log2f(lt));
   }
   E* go = reinterpret_cast<E*>(p.o.p) + b * p.o.sb + (int64_t)qrow * p.o.st + hh * p.o.sh;
-  float* gob = reinterpret_cast<float*>(p.obr.p) + b * p.obr.sb + (int64_t)qrow * p.obr.st + hh * p.obr.sh;
+  float* gob = reinterpret_cast<float*>(p.obr.p) + b * p.obr.sb + (int64_t)qrow * p.obr.st + hh * p.obr.sh + br * p.obr.si;
 #pragma unroll
   for (int d = 0; d < NDB; ++d)
 #pragma unroll
@@ -3208,10 +3264,10 @@ void attn_fwd3_kernel(FwdParams p) {
         const float a0 = acc[i][d][4 * g + 0] * inv[i], a1 = acc[i][d][4 * g + 1] * inv[i];
         const float a2 = acc[i][d][4 * g + 2] * inv[i], a3 = acc[i][d][4 * g + 3] * inv[i];
         store4<float>(gob + i * p.obr.si + e, a0, a1, a2, a3);
-        const float c = p.coef[hh * p.cst + i];
+        const float c = nsp > 1 ? 1.f : p.coef[hh * p.cst + i];
         o0 = fmaf(c, a0, o0); o1 = fmaf(c, a1, o1); o2 = fmaf(c, a2, o2); o3 = fmaf(c, a3, o3);
       }
-      store4<E>(go + e, o0, o1, o2, o3);
+      if (nsp == 1) store4<E>(go + e, o0, o1, o2, o3);
     }
 }
 
@@ -3552,6 +3608,8 @@ void attn_dkdv2_kernel(BwdParams p) {
   for (int t = tfull; t < ttail; ++t) step(t, std::false_type{}, true);
   for (int t = ttail; t < nsteps; ++t) step(t, std::true_type{}, true);
   dq2_acc_fence();
+  acc_pin(dk);
+  acc_pin(dv);
 
   if (!wave_keys || krow >= T) return;
   E* gdk = reinterpret_cast<E*>(p.dk.p) + b * p.dk.sb + (int64_t)krow * p.dk.st + hh * p.dk.sh;
@@ -3688,7 +3746,11 @@ int launch_fwd_t(const FwdParams& p, hipStream_t st) {
   } else {
   if constexpr (Fw3Cfg<E, HS, N, PL::DV>::ok && !DROP) {
     // one wave per SIMD, key tiles software-pipelined (attn_fwd3_kernel, unit attn_bf16_dq2.hip)
-    if (p.bsplit <= 1 && kv_layout_ok(p, (int)sizeof(E)) && fwd3_env()) return launch_attn_fwd3_bf16(p, st);
+    if (kv_layout_ok(p, (int)sizeof(E)) && fwd3_env()) {
+      FwdParams q = p;
+      q.N = N;            // a branch-split launch runs the N = 1 instance with p.N = the call's N
+      return launch_attn_fwd3_bf16(q, st);
+    }
   }
   if constexpr (Fw2Cfg<E, HS, N, PL::DV>::ok && !DROP) {
     // one wave per SIMD, two 32-row blocks per wave (attn_fwd2_kernel, unit attn_bf16_dq2.hip)
@@ -3735,7 +3797,8 @@ int launch_fwd3_t(const FwdParams& p, hipStream_t st) {
   using C3 = Fw3Cfg<E, HS, N, DV>;
   auto kern = attn_fwd3_kernel<E, HS, N, DV>;
   if (int e = set_smem(kern, C3::bytes)) return e;
-  hipLaunchKernelGGL(kern, dim3((p.T + C3::BM - 1) / C3::BM, p.H, p.B), dim3(256), C3::bytes, st, p);
+  const int nsp = (N == 1 && p.bsplit > 1) ? p.bsplit : 1;
+  hipLaunchKernelGGL(kern, dim3((p.T + C3::BM - 1) / C3::BM, p.H * nsp, p.B), dim3(256), C3::bytes, st, p);
   return (int)hipGetLastError();
 }
 // DTA_FWD3 = 1 in the environment selects attn_fwd3_kernel where it is built

@@ -20,15 +20,31 @@ template <class E> struct Vec8;
 template <> struct Vec8<__bf16> { typedef bf16x8 t; };
 template <> struct Vec8<_Float16> { typedef f16x8 t; };
 
+// streaming policy of the row-wise kernels' activations (read once, written once):
+// bit 0 = non-temporal loads, bit 1 = non-temporal stores
+#ifndef DTA_EW_NT
+#define DTA_EW_NT 0
+#endif
+template <class V>
+__device__ __forceinline__ V ldv(const V* p) {
+  if constexpr (DTA_EW_NT & 1) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+template <class V>
+__device__ __forceinline__ void stv(V* p, V v) {
+  if constexpr (DTA_EW_NT & 2) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
 // load/store 8 consecutive elements as fp32
 template <class E>
 __device__ __forceinline__ void ld8(const E* p, float* f) {
   if constexpr (sizeof(E) == 2) {
-    typename Vec8<E>::t v = *reinterpret_cast<const typename Vec8<E>::t*>(p);
+    typename Vec8<E>::t v = ldv(reinterpret_cast<const typename Vec8<E>::t*>(p));
 #pragma unroll
     for (int j = 0; j < 8; ++j) f[j] = (float)v[j];
   } else {
-    f32x4 a = *reinterpret_cast<const f32x4*>(p), b = *reinterpret_cast<const f32x4*>(p + 4);
+    f32x4 a = ldv(reinterpret_cast<const f32x4*>(p)), b = ldv(reinterpret_cast<const f32x4*>(p + 4));
 #pragma unroll
     for (int j = 0; j < 4; ++j) { f[j] = a[j]; f[j + 4] = b[j]; }
   }
@@ -39,10 +55,10 @@ __device__ __forceinline__ void st8(E* p, const float* f) {
     typename Vec8<E>::t v;
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = (E)f[j];
-    *reinterpret_cast<typename Vec8<E>::t*>(p) = v;
+    stv(reinterpret_cast<typename Vec8<E>::t*>(p), v);
   } else {
-    *reinterpret_cast<f32x4*>(p) = f32x4{f[0], f[1], f[2], f[3]};
-    *reinterpret_cast<f32x4*>(p + 4) = f32x4{f[4], f[5], f[6], f[7]};
+    stv(reinterpret_cast<f32x4*>(p), f32x4{f[0], f[1], f[2], f[3]});
+    stv(reinterpret_cast<f32x4*>(p + 4), f32x4{f[4], f[5], f[6], f[7]});
   }
 }
 
@@ -136,7 +152,7 @@ template <class E> struct Raw8 { typedef s16x8 t; };
 template <> struct Raw8<float> { typedef f32x4 t[2]; };
 
 template <class E>
-__device__ __forceinline__ void raw_ld(const E* p, s16x8& v) { v = *reinterpret_cast<const s16x8*>(p); }
+__device__ __forceinline__ void raw_ld(const E* p, s16x8& v) { v = ldv(reinterpret_cast<const s16x8*>(p)); }
 template <class E>
 __device__ __forceinline__ void raw_cvt(const s16x8& v, float* f) {
   const typename Vec8<E>::t w = __builtin_bit_cast(typename Vec8<E>::t, v);
@@ -421,25 +437,39 @@ __global__ __launch_bounds__(256) void ln_bwd_reduce2_kernel(const float* part2,
 }
 
 
-// one thread = 4 rotation pairs (8 elements)
+// 32-bit division by a launch constant: q = (umulhi(x, m) + x) >> s, exact for x < 2^31
+// (round-up multiplier; the element index of a launch stays below 2^31 on this path)
+struct FastDiv {
+  uint32_t d, m, s;
+  FastDiv() = default;
+  explicit FastDiv(uint32_t d_) : d(d_), m(0), s(0) {
+    while ((1ull << s) < d) ++s;
+    m = (uint32_t)((((1ull << s) - d) << 32) / d + 1);
+  }
+  __device__ __forceinline__ uint32_t div(uint32_t x) const { return (__umulhi(x, m) + x) >> s; }
+};
+struct RopeDiv { FastDiv row, T, per_row, N; uint32_t rowlen; };
+
+// one thread = 4 rotation pairs (8 elements); the 64-bit index decomposition of the first
+// version (five int64 div/mod per thread) cost more VALU than the HBM time of its 32 bytes
 template <class E, class S>
-__global__ __launch_bounds__(256) void rope_kernel(RopeParams p) {
-  const int per_row = p.HS / 8;
-  const int64_t total = (int64_t)p.B * p.T * p.H * p.N * per_row;
-  for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * 256) {
-    int64_t r = idx;
-    const int c = r % per_row; r /= per_row;
-    const int i = r % p.N; r /= p.N;
-    const int h = r % p.H; r /= p.H;
-    const int t = r % p.T; const int b = (int)(r / p.T);
+__global__ __launch_bounds__(256) void rope_kernel(RopeParams p, RopeDiv dv) {
+  const uint32_t total = (uint32_t)p.B * p.T * p.H * p.N * (p.HS / 8);
+  for (uint32_t idx = blockIdx.x * 256 + threadIdx.x; idx < total; idx += gridDim.x * 256) {
+    const uint32_t row = dv.row.div(idx), within = idx - row * dv.rowlen;
+    const uint32_t b = dv.T.div(row), t = row - b * p.T;
+    const uint32_t hi = dv.per_row.div(within), c = within - hi * dv.per_row.d;
+    const uint32_t h = dv.N.div(hi), i = hi - h * p.N;
     const S* src = reinterpret_cast<const S*>(p.src.p) + b * p.src.sb + (int64_t)t * p.src.st + h * p.src.sh + i * p.src.si + c * 8;
     E* dst = reinterpret_cast<E*>(p.dst.p) + b * p.dst.sb + (int64_t)t * p.dst.st + h * p.dst.sh + i * p.dst.si + c * 8;
     float x[8], o[8];
     ld8<S>(src, x);
     const float* f = p.freqs + ((int64_t)t * (p.HS / 2) + c * 4) * 2;
+    const f32x4 f0 = *reinterpret_cast<const f32x4*>(f), f1 = *reinterpret_cast<const f32x4*>(f + 4);
+    const float fr[8] = {f0[0], f0[1], f0[2], f0[3], f1[0], f1[1], f1[2], f1[3]};
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const float cs = f[2 * j], sn = p.inverse ? -f[2 * j + 1] : f[2 * j + 1];
+      const float cs = fr[2 * j], sn = p.inverse ? -fr[2 * j + 1] : fr[2 * j + 1];
       const float a = x[2 * j], bb = x[2 * j + 1];
       o[2 * j] = a * cs - bb * sn;          // (a + ib)(cos + i sin)
       o[2 * j + 1] = a * sn + bb * cs;
@@ -555,10 +585,17 @@ int launch_ln(int dtype, const LnParams& p, bool bwd, hipStream_t st) {
 int launch_rope(int dtype, bool src_f32, const RopeParams& p, hipStream_t st) {
   const int64_t items = (int64_t)p.B * p.T * p.H * p.N * (p.HS / 8);
   if (items == 0) return 0;
+  if (items >= (1ll << 31) || p.HS % 8) return -2;
+  RopeDiv dv;
+  dv.rowlen = (uint32_t)(p.H * p.N * (p.HS / 8));
+  dv.row = FastDiv(dv.rowlen);
+  dv.T = FastDiv((uint32_t)p.T);
+  dv.per_row = FastDiv((uint32_t)(p.HS / 8));
+  dv.N = FastDiv((uint32_t)p.N);
   dim3 g(grid_for(items));
 #define DTA_R(E_)                                                                         \
-  if (src_f32) hipLaunchKernelGGL((rope_kernel<E_, float>), g, dim3(256), 0, st, p);       \
-  else hipLaunchKernelGGL((rope_kernel<E_, E_>), g, dim3(256), 0, st, p);
+  if (src_f32) hipLaunchKernelGGL((rope_kernel<E_, float>), g, dim3(256), 0, st, p, dv);   \
+  else hipLaunchKernelGGL((rope_kernel<E_, E_>), g, dim3(256), 0, st, p, dv);
   switch (dtype) {
     case 0: DTA_R(__bf16) break;
     case 1: DTA_R(_Float16) break;

@@ -33,18 +33,27 @@ def main():
         lib.dta_ln_fwd.argtypes = lib.dta_ln_bwd.argtypes = [ctypes.POINTER(_lib.LnArgs), ctypes.c_void_p]
         lib.dta_ln_bwd_workspace_bytes.argtypes = [ctypes.c_int64] * 2
         lib.dta_ln_bwd_workspace_bytes.restype = ctypes.c_size_t
+        lib.dta_rope.argtypes = [ctypes.POINTER(_lib.RopeArgs), ctypes.c_void_p]
         libs[name] = lib
+    # RoPE of every Q_i / K_i at cfg3 (bench.py hbm_bench's rope shape)
+    Br, Tr, H2, Nr, hr = 16, 2048, 12, 3, 64
+    rsrc = torch.randn(Br, Tr, H2, Nr, hr, device=dev, generator=g).to(torch.bfloat16)
+    rdst = torch.empty_like(rsrc)
+    from differential_transformer_replication_amd.Ndiff_transformer import precompute_freqs_cis
+    table = torch.view_as_real(precompute_freqs_cis(hr, Tr)).to(dev).contiguous()
+    ra = _lib.RopeArgs(_lib.DTA_BF16, Br, Tr, H2, Nr, hr, 0, 0, _lib.tensor5(rsrc), _lib.tensor5(rdst), table.data_ptr())
     part = torch.empty(max(l.dta_ln_bwd_workspace_bytes(rows, C) for l in libs.values()) // 4, device=dev)
     fa = _lib.LnArgs(_lib.DTA_BF16, rows, C, 1e-5, 0.2, x.data_ptr(), C, y.data_ptr(), C, w.data_ptr(),
                      b.data_ptr(), mean.data_ptr(), rstd.data_ptr(), None, 0, None, 0, None, None)
     ba = _lib.LnArgs(_lib.DTA_BF16, rows, C, 1e-5, 0.2, x.data_ptr(), C, None, 0, w.data_ptr(), None,
                      mean.data_ptr(), rstd.data_ptr(), dy.data_ptr(), C, dx.data_ptr(), C, dw.data_ptr(),
                      db.data_ptr(), part.data_ptr())
-    times = {n: {"fwd": [], "bwd": []} for n in libs}
+    times = {n: {"fwd": [], "bwd": [], "rope": []} for n in libs}
     ref = None
     for rnd in range(6):
         for n, lib in libs.items():
-            for kind, fn in (("fwd", lambda: lib.dta_ln_fwd(fa, stream)), ("bwd", lambda: lib.dta_ln_bwd(ba, stream))):
+            for kind, fn in (("fwd", lambda: lib.dta_ln_fwd(fa, stream)), ("bwd", lambda: lib.dta_ln_bwd(ba, stream)),
+                             ("rope", lambda: lib.dta_rope(ra, stream))):
                 for _ in range(2):
                     fn()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -56,14 +65,17 @@ def main():
                 times[n][kind].append(e0.elapsed_time(e1) / 10 * 1e3)
             if rnd == 0:
                 if ref is None:
-                    ref = dx.clone()
+                    ref = (dx.clone(), y.clone(), rdst.clone())
                 else:
-                    times[n]["dx_equal"] = bool(torch.equal(ref, dx))
+                    times[n]["dx_equal"] = bool(torch.equal(ref[0], dx))
+                    times[n]["y_equal"] = bool(torch.equal(ref[1], y))
+                    times[n]["rope_equal"] = bool(torch.equal(ref[2], rdst))
     out = {}
     for n, d in times.items():
         out[n] = {k: (sorted(v)[len(v) // 2] if isinstance(v, list) else v) for k, v in d.items()}
         out[n]["bwd_TBps"] = 3 * rows * C * 2 / out[n]["bwd"] / 1e6
         out[n]["fwd_TBps"] = 2 * rows * C * 2 / out[n]["fwd"] / 1e6
+        out[n]["rope_TBps"] = 2 * rsrc.numel() * 2 / out[n]["rope"] / 1e6
     print(json.dumps(out))
 
 

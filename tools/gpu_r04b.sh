@@ -25,3 +25,7 @@ if [ -n "$SQ" ]; then
   python3 $R/tools/pmc_sq.py $R/$OUT/sq/p* --json $R/$OUT/sq.json > $R/$OUT/sq.txt && tail -40 $R/$OUT/sq.txt
   cd $R
 fi
+if [ -n "$LNAB" ]; then
+  cd $R && timeout -k 10 200 python tools/ab_ln.py $LNAB > $OUT/ab_ln.json 2> $OUT/ab_ln.err || { echo LNAB_FAILED; tail -5 $OUT/ab_ln.err; exit 1; }
+  cat $OUT/ab_ln.json
+fi
