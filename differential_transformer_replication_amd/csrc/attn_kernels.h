@@ -1513,9 +1513,23 @@ void attn_dq_kernel(BwdParams p) {
 // waits before reading the accumulators (dq2_acc_fence).
 template <bool NOP>
 __device__ __forceinline__ void mfma_agpr(f32x16& acc, bf16x8 a, bf16x8 b) {
-  if constexpr (NOP) asm("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
-  else asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+  if constexpr (NOP) asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+  else asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
 }
+// The compiler also does not see that an asm MFMA is still reading its A / B VGPRs after it
+// issues: it may hand them to the next VALU result at once (a first attn_fwd3 build wrote a
+// branch condition into a V fragment one instruction after the MFMA that read it).  Every
+// asm MFMA of a stream therefore keeps the previous one's operands alive until it has
+// itself issued; mfma_release after the stream's fence ends the last pair.
+struct MfmaHold { bf16x8 a, b; };
+template <bool NOP>
+__device__ __forceinline__ void mfma_agpr(f32x16& acc, bf16x8 a, bf16x8 b, MfmaHold& h) {
+  mfma_agpr<NOP>(acc, a, b);
+  asm volatile("" ::"v"(h.a), "v"(h.b));
+  h.a = a;
+  h.b = b;
+}
+__device__ __forceinline__ void mfma_release(const MfmaHold& h) { asm volatile("" ::"v"(h.a), "v"(h.b)); }
 __device__ __forceinline__ void dq2_acc_fence() { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory"); }
 // pin accumulators after a fence: their readers (v_accvgpr_read, allocator copies) then
 // depend on the pins, which volatile ordering keeps after the fence's wait states
@@ -1762,6 +1776,7 @@ void attn_dq2_kernel(BwdParams p) {
   lds_barrier();
 
   f32x16 dq[2][N][NHB];
+  MfmaHold hold{};
 #pragma unroll
   for (int qb = 0; qb < 2; ++qb)
 #pragma unroll
@@ -1849,7 +1864,7 @@ void attn_dq2_kernel(BwdParams p) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(tr[j]));
         }
-        mfma_agpr<(s == SCH::v.c0[o.u])>(dq[o.qb][o.i][o.a], tr_frag<E>(tr, o.c), pk[o.u][o.b * 2 + o.c]);
+        mfma_agpr<(s == SCH::v.c0[o.u])>(dq[o.qb][o.i][o.a], tr_frag<E>(tr, o.c), pk[o.u][o.b * 2 + o.c], hold);
       }
       sfor<SCH::v.npiece[s]>([&](auto K) { piece(std::integral_constant<int, SCH::v.pu[s][decltype(K)::value]>{}); });
       __builtin_amdgcn_sched_barrier(0);
@@ -1871,6 +1886,7 @@ void attn_dq2_kernel(BwdParams p) {
   for (int kt = nlive; kt < ntiles; ++kt) step(kt, std::false_type{}, false);
   dq2_acc_fence();
   acc_pin(dq);
+  mfma_release(hold);
 
 #pragma unroll
   for (int qb = 0; qb < 2; ++qb) {
@@ -2575,6 +2591,7 @@ void attn_fwd2_kernel(FwdParams p) {
   for (int i = 0; i < N; ++i) stage<E, HS, BM, HS, NTHR>(Qs + i * BM * HS, gq + i * p.q.si, p.q.st, q0, T - 1, tid);
 
   f32x16 acc[U][NDB];
+  MfmaHold hold{};
   float m[U], l[U];
   float bad = 0.f;
   const bool wave_live = qw0 < T;
@@ -2612,8 +2629,8 @@ void attn_fwd2_kernel(FwdParams p) {
       lgkm_pin<NKB>(r);
 #pragma unroll
       for (int kb = 0; kb < NKB; ++kb) {
-        mfma_agpr<true>(acc[u][d], tr_frag<E>(r[kb], 0), pk[kb * 2 + 0]);
-        mfma_agpr<false>(acc[u][d], tr_frag<E>(r[kb], 1), pk[kb * 2 + 1]);
+        mfma_agpr<true>(acc[u][d], tr_frag<E>(r[kb], 0), pk[kb * 2 + 0], hold);
+        mfma_agpr<false>(acc[u][d], tr_frag<E>(r[kb], 1), pk[kb * 2 + 1], hold);
       }
     });
   };
@@ -2721,7 +2738,7 @@ void attn_fwd2_kernel(FwdParams p) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(tr[j]));
         }
-        mfma_agpr<(s == SCH::v.p0[o.u])>(acc[o.u][o.a], tr_frag<E>(tr, o.c), pk[o.u % SD::PR][o.b * 2 + o.c]);
+        mfma_agpr<(s == SCH::v.p0[o.u])>(acc[o.u][o.a], tr_frag<E>(tr, o.c), pk[o.u % SD::PR][o.b * 2 + o.c], hold);
       }
       sfor<SCH::v.npiece[s]>([&](auto K) { piece(std::integral_constant<int, SCH::v.pu[s][decltype(K)::value]>{}); });
       __builtin_amdgcn_sched_barrier(0);
@@ -2799,6 +2816,7 @@ void attn_fwd2_kernel(FwdParams p) {
   }
   dq2_acc_fence();
   acc_pin(acc);
+  mfma_release(hold);
 
   if (!wave_live) return;
 #pragma unroll
@@ -2983,6 +3001,7 @@ void attn_fwd3_kernel(FwdParams p) {
       asm volatile("" : "+a"(qf[i][s]));
     }
   f32x16 acc[N][NDB];
+  MfmaHold hold{};
   float m[N], l[N];
   float bad = 0.f;
   const bool wave_live = qw0 < T;
@@ -3113,7 +3132,7 @@ void attn_fwd3_kernel(FwdParams p) {
 #pragma unroll
           for (int q = 0; q < 4; ++q) asm volatile("" : "+v"(tr[q]));
         }
-        mfma_agpr<(o.b == 0 && o.c == 0)>(acc[o.i][o.a], tr_frag<E>(tr, o.c), pk[o.i][o.b * 2 + o.c]);
+        mfma_agpr<(o.b == 0 && o.c == 0)>(acc[o.i][o.a], tr_frag<E>(tr, o.c), pk[o.i][o.b * 2 + o.c], hold);
       }
       sfor<SCH::v.npiece[s]>([&](auto K) { piece(std::integral_constant<int, SCH::v.pp[s][decltype(K)::value]>{}); });
       __builtin_amdgcn_sched_barrier(0);
@@ -3124,6 +3143,7 @@ void attn_fwd3_kernel(FwdParams p) {
     // merge, the last MFMA must have landed
     dq2_acc_fence();
     acc_pin(acc);
+    mfma_release(hold);
   };
 
   for (int pass = 0; pass < 2; ++pass) {
@@ -3242,6 +3262,7 @@ void attn_fwd3_kernel(FwdParams p) {
   }
   dq2_acc_fence();
   acc_pin(acc);
+  mfma_release(hold);
 
   if (!wave_live || qrow >= T) return;
   float inv[N];
@@ -3481,6 +3502,7 @@ void attn_dkdv2_kernel(BwdParams p) {
   lds_barrier();
 
   f32x16 dk[N][NHB], dv[NVB];
+  MfmaHold hold{};
 #pragma unroll
   for (int i = 0; i < N; ++i)
 #pragma unroll
@@ -3583,9 +3605,9 @@ void attn_dkdv2_kernel(BwdParams p) {
           for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(tr[j]));
         }
         if constexpr (o.kind == kv2::CK)
-          mfma_agpr<(s == SCH::v.c0[o.u])>(dk[o.i][o.a], tr_frag<E>(tr, o.c), dsp[o.u][o.c]);
+          mfma_agpr<(s == SCH::v.c0[o.u])>(dk[o.i][o.a], tr_frag<E>(tr, o.c), dsp[o.u][o.c], hold);
         else
-          mfma_agpr<(s == SCH::v.v0[o.qs])>(dv[o.a], tr_frag<E>(tr, o.c), pcp[o.qs][o.c]);
+          mfma_agpr<(s == SCH::v.v0[o.qs])>(dv[o.a], tr_frag<E>(tr, o.c), pcp[o.qs][o.c], hold);
       }
       sfor<SCH::v.npiece[s]>([&](auto K) { piece(std::integral_constant<int, SCH::v.pu[s][decltype(K)::value]>{}); });
       __builtin_amdgcn_sched_barrier(0);
@@ -3610,6 +3632,7 @@ void attn_dkdv2_kernel(BwdParams p) {
   dq2_acc_fence();
   acc_pin(dk);
   acc_pin(dv);
+  mfma_release(hold);
 
   if (!wave_keys || krow >= T) return;
   E* gdk = reinterpret_cast<E*>(p.dk.p) + b * p.dk.sb + (int64_t)krow * p.dk.st + hh * p.dk.sh;

@@ -29,18 +29,36 @@ def scan(text):
         lines = [ln.split(";")[0].strip() for ln in text[m.end():end].split("\n")]
         lines = [ln for ln in lines if ln and not ln.startswith(".") and not ln.endswith(":")]
         cyc, written, hazards, scratch = 0, {}, [], 0
+        reading, read_at = set(), 0   # VGPRs an asm MFMA (AGPR destination) may still be reading
         for ln in lines:
             parts = ln.replace(",", " ").split()
             op = parts[0]
             if op.startswith("scratch_"):
                 scratch += 1
             cyc += int(parts[1]) + 1 if op == "s_nop" else 1
+            if op.startswith(("s_waitcnt", "s_barrier")):
+                cyc += 16                  # at least that long, in practice far longer
+            if reading and cyc - read_at > WAIT_STATES:
+                reading = set()            # the MFMA has read its operands by now
             if op.startswith("v_mfma"):
+                reading, read_at = set(), cyc
                 d = re.match(r"a\[(\d+):(\d+)\]", parts[1])
                 if d:
                     for r in range(int(d.group(1)), int(d.group(2)) + 1):
                         written[r] = cyc
+                    for o in parts[2:4]:
+                        v = re.match(r"v\[(\d+):(\d+)\]$", o)
+                        if v:
+                            reading.update(range(int(v.group(1)), int(v.group(2)) + 1))
                 continue
+            # write-after-read: a VGPR source of the last asm MFMA overwritten before the
+            # next MFMA issues (LDS reads excepted: their data returns >= 64 cycles later)
+            if reading and op.startswith("v_") and len(parts) > 1:
+                v = re.match(r"v(\d+)$", parts[1]) or re.match(r"v\[(\d+):(\d+)\]$", parts[1])
+                if v:
+                    regs = [int(v.group(1))] if v.lastindex == 1 else range(int(v.group(1)), int(v.group(2)) + 1)
+                    if any(r in reading for r in regs):
+                        hazards.append("WAR " + ln)
             for o in (parts[1:] if op.startswith(STORES) else parts[2:]):
                 a = re.match(r"a(\d+)$", o) or re.match(r"a\[(\d+):(\d+)\]$", o)
                 if not a:

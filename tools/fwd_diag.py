@@ -57,7 +57,7 @@ def main():
         outs = [run_fwd(lib, q, k, v, coef, B, T, H, N, hs, dv, dev, stream) for _, lib in libs]
         (o1, b1, l1), (o2, b2, l2) = outs
         scale = b2.abs().max().item()
-        d = (b1 - b2).abs() / scale                               # [N][B][T][H][dv]
+        d = torch.nan_to_num((b1 - b2).abs() / scale, nan=9.0)  # [N][B][T][H][dv]
         nrb = (T + 31) // 32
         per_rows = [round(d[:, :, 32 * r:32 * r + 32].max().item(), 4) for r in range(nrb)]
         per_branch = [round(d[i].max().item(), 4) for i in range(N)]
@@ -65,7 +65,11 @@ def main():
         per_row_in_blk = [round(d[:, :, [t for t in range(T) if t % 32 == r]].max().item(), 4) for r in range(32)]
         dl = (l1 - l2).abs()                                      # [N][B][H][T]
         lse_rows = [round(dl[..., 32 * r:32 * r + 32].max().item(), 4) for r in range(nrb)]
-        res[sh] = {"o": round(((o1 - o2).abs().max() / o2.abs().max()).item(), 5), "obr_branch": per_branch,
+        nanrows = sorted(set(torch.nonzero(~torch.isfinite(b1).all(dim=-1).all(dim=-1).all(dim=0).all(dim=0))[:, 0].tolist())) if False else \
+            sorted(set(torch.nonzero((~torch.isfinite(b1)).any(dim=-1).any(dim=-1).any(dim=0).any(dim=0))[:, 0].tolist()))
+        d = torch.nan_to_num(d, nan=9.0)
+        res[sh] = {"nan_rows": nanrows[:40], "n_nan_rows": len(nanrows),
+                   "o": round(((o1 - o2).abs().max() / o2.abs().max()).item(), 5), "obr_branch": per_branch,
                    "obr_rowblk": per_rows, "obr_colblk": per_col, "obr_row_mod32": per_row_in_blk,
                    "lse_rowblk": lse_rows, "finite": bool(torch.isfinite(b1).all().item())}
         print(sh, json.dumps(res[sh]), flush=True)
