@@ -1701,8 +1701,10 @@ void attn_dq2_kernel(BwdParams p) {
   using KR = KvRing<E, HS, N, DV, BN, NW>;
   uint32_t doff[KR::MYP];
   KR::offsets(p.k.st, p.k.si, p.v.st, wave, lane, doff);
+  // past the last tile a null tile (no rows: zeros into a free slot): no branch in the
+  // stream, constant vmcnt waits
   auto stage_kv = [&](int kt, int buf) {
-    KR::issue_pre(gk, p.k.st, gv, p.v.st, kt * BN, T, Kb + buf * CF::nK, Vb + buf * CF::nV, wave, doff);
+    KR::issue_pre(gk, p.k.st, gv, p.v.st, kt * BN, kt < ntiles ? T : 0, Kb + buf * CF::nK, Vb + buf * CF::nV, wave, doff);
   };
 
   // ---- per-block row operands: dO rows (B operands of dP), delta, LSE seeds
@@ -1768,9 +1770,8 @@ void attn_dq2_kernel(BwdParams p) {
 #pragma unroll
   for (int i = 0; i < N; ++i) stage<E, HS, BM, HS, NTHR>(Qs + i * BM * HS, gq + i * p.q.si, p.q.st, q0, T - 1, tid);
   const int tile_pieces = KR::pieces(wave);
-  for (int j = 0; j < NS - 1; ++j)
-    if (j < ntiles) stage_kv(j, j);
-  wait_vm(tile_pieces * max(0, min(NS - 1, ntiles) - 1));
+  for (int j = 0; j < NS - 1; ++j) stage_kv(j, j);
+  wait_vm(tile_pieces * (NS - 2));
   lds_barrier();
   scale_lds<E, NTHR>(Qs, CF::nQ, p.sl2, tid);
   lds_barrier();
@@ -1840,9 +1841,8 @@ void attn_dq2_kernel(BwdParams p) {
       sfor<KR::MYP>([&](auto U) {
         constexpr int u = decltype(U)::value;
         if constexpr (s == (u + 1) * NOPS / (KR::MYP + 1))
-          if (kt_dma < ntiles)
-            KR::template issue_one<u>(gk, p.k.st, gv, p.v.st, kt_dma * BN, T, Kb + (kt_dma % NS) * CF::nK,
-                                      Vb + (kt_dma % NS) * CF::nV, wave, doff[u]);
+          KR::template issue_one<u>(gk, p.k.st, gv, p.v.st, kt_dma * BN, kt_dma < ntiles ? T : 0,
+                                    Kb + (kt_dma % NS) * CF::nK, Vb + (kt_dma % NS) * CF::nV, wave, doff[u]);
       });
       if constexpr (SCH::v.nreads[s] > 0) lgkm_wait<SCH::v.pending(s, R)>();
       if constexpr (o.kind == dq2::SS) {
@@ -1872,8 +1872,8 @@ void attn_dq2_kernel(BwdParams p) {
   };
   auto step = [&](int kt, auto MASKED, bool live) {
     if (live) body(kt, MASKED, kt + NS - 1);
-    else if (kt + NS - 1 < ntiles) stage_kv(kt + NS - 1, (kt + NS - 1) % NS);
-    wait_vm(tile_pieces * max(0, min(NS - 2, ntiles - 2 - kt)));
+    else stage_kv(kt + NS - 1, (kt + NS - 1) % NS);
+    wait_vm(tile_pieces * (NS - 2));
     lds_barrier();
   };
   // per wave: tiles wholly below its first row, its diagonal / ragged tiles, then tiles past
@@ -2925,6 +2925,9 @@ struct Hold { static constexpr Sched<N, NSQ, NDB, HAS_S, HAS_V> v{}; };
 #ifndef DTA_FWD3
 #define DTA_FWD3 1
 #endif
+#ifndef DTA_FWD3_SPREAD
+#define DTA_FWD3_SPREAD 1      // LDS-DMA pieces spread over the stream (0: one burst per tile)
+#endif
 template <class E, int HS, int N, int DV>
 struct Fw3Cfg {
   static constexpr int NW = 4, BM = 128, BN = 64, NS = 5;
@@ -2980,16 +2983,16 @@ void attn_fwd3_kernel(FwdParams p) {
   using KR = KvRing<E, HS, N, DV, BN, NW>;
   uint32_t doff[KR::MYP];
   KR::offsets(p.k.st, p.k.si, p.v.st, wave, lane, doff);
+  // every iteration issues one tile: past the last one a null tile (no rows: the DMA reads
+  // nothing and writes zeros into a free slot), so the stream carries no branch and every
+  // vmcnt is a constant
   auto stage_kv = [&](int kt) {
-    if (kt < ntiles) KR::issue_pre(gk, p.k.st, gv, p.v.st, kt * BN, T, Kb + (kt % NS) * CF::nK, Vb + (kt % NS) * CF::nV, wave, doff);
+    KR::issue_pre(gk, p.k.st, gv, p.v.st, kt * BN, kt < ntiles ? T : 0, Kb + (kt % NS) * CF::nK, Vb + (kt % NS) * CF::nV,
+                  wave, doff);
   };
   const int tile_pieces = KR::pieces(wave);
   // vmcnt such that tile `need` has landed when every tile up to `issued` was issued
-  auto wait_tiles = [&](int need, int issued) {
-    issued = min(issued, ntiles - 1);
-    need = min(need, ntiles - 1);
-    wait_vm(tile_pieces * max(0, issued - need));
-  };
+  auto wait_tiles = [&](int need, int issued) { wait_vm(tile_pieces * (issued - need)); };
 
   // this wave's Q_i rows: B operands of S^T = K_i Q_i^T, in AGPRs
   frag qf[N][NSQ];
@@ -3105,6 +3108,7 @@ void attn_fwd3_kernel(FwdParams p) {
       constexpr int k = decltype(K_)::value, i = k / 4, x = k % 4;
       pk[i][x] = O::template pack<x % 2>(sa[CUR][i][x / 2]);
     };
+    if constexpr (!DTA_FWD3_SPREAD) stage_kv(kt_dma);
     sfor<(R < NOPS ? R : NOPS)>([&](auto S_) { issue(S_); });
     sfor<NOPS>([&](auto S_) {
       constexpr int s = decltype(S_)::value;
@@ -3114,10 +3118,9 @@ void attn_fwd3_kernel(FwdParams p) {
       // burst they held the MFMAs for ~60+ cycles each)
       sfor<KR::MYP>([&](auto U) {
         constexpr int u = decltype(U)::value;
-        if constexpr (s == (u + 1) * NOPS / (KR::MYP + 1))
-          if (kt_dma < ntiles)
-            KR::template issue_one<u>(gk, p.k.st, gv, p.v.st, kt_dma * BN, T, Kb + (kt_dma % NS) * CF::nK,
-                                      Vb + (kt_dma % NS) * CF::nV, wave, doff[u]);
+        if constexpr (DTA_FWD3_SPREAD && s == (u + 1) * NOPS / (KR::MYP + 1))
+          KR::template issue_one<u>(gk, p.k.st, gv, p.v.st, kt_dma * BN, kt_dma < ntiles ? T : 0,
+                                    Kb + (kt_dma % NS) * CF::nK, Vb + (kt_dma % NS) * CF::nV, wave, doff[u]);
       });
       sfor<SCH::v.npack[s]>([&](auto K) { pack(std::integral_constant<int, SCH::v.pkk[s][decltype(K)::value]>{}); });
       if constexpr (SCH::v.nreads[s] > 0) lgkm_wait<SCH::v.pending(s, R)>();

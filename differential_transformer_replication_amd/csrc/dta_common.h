@@ -211,12 +211,17 @@ __device__ __forceinline__ void stage_vec(E* dst, const E* src, bool valid) {
 // Store 4 consecutive accumulator values (registers 4g..4g+3) as elements.
 template <class E>
 __device__ __forceinline__ void store4(E* dst, float a, float b, float c, float d) {
+#ifndef DTA_ATTN_NT
+#define DTA_ATTN_NT 0          // 1: the attention epilogues' global stores non-temporal
+#endif
   if constexpr (sizeof(E) == 2) {
     typedef E v4 __attribute__((ext_vector_type(4)));
     v4 v = {(E)a, (E)b, (E)c, (E)d};
-    *reinterpret_cast<v4*>(dst) = v;
+    if constexpr (DTA_ATTN_NT) __builtin_nontemporal_store(v, reinterpret_cast<v4*>(dst));
+    else *reinterpret_cast<v4*>(dst) = v;
   } else {
-    *reinterpret_cast<f32x4*>(dst) = f32x4{a, b, c, d};
+    if constexpr (DTA_ATTN_NT) __builtin_nontemporal_store(f32x4{a, b, c, d}, reinterpret_cast<f32x4*>(dst));
+    else *reinterpret_cast<f32x4*>(dst) = f32x4{a, b, c, d};
   }
 }
 

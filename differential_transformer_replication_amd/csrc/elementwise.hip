@@ -21,9 +21,12 @@ template <> struct Vec8<__bf16> { typedef bf16x8 t; };
 template <> struct Vec8<_Float16> { typedef f16x8 t; };
 
 // streaming policy of the row-wise kernels' activations (read once, written once):
-// bit 0 = non-temporal loads, bit 1 = non-temporal stores
+// bit 0 = non-temporal loads, bit 1 = non-temporal stores.  One-process A/B at cfg2's
+// GroupLayerNorm and cfg3's RoPE (profiles/r04_ab_ln_nt.json): nt stores 45.6 -> 41.7 us
+// (ln_fwd, 6.44 TB/s), 90.3 -> 76.6 (ln_bwd), 51.3 -> 42.2 (rope, 7.15 TB/s); nt loads
+// slower (52.6 us ln_fwd) with or without them.  Outputs bitwise equal.
 #ifndef DTA_EW_NT
-#define DTA_EW_NT 0
+#define DTA_EW_NT 2
 #endif
 template <class V>
 __device__ __forceinline__ V ldv(const V* p) {

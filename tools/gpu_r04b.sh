@@ -29,3 +29,14 @@ if [ -n "$LNAB" ]; then
   cd $R && timeout -k 10 200 python tools/ab_ln.py $LNAB > $OUT/ab_ln.json 2> $OUT/ab_ln.err || { echo LNAB_FAILED; tail -5 $OUT/ab_ln.err; exit 1; }
   cat $OUT/ab_ln.json
 fi
+if [ -n "$FULL" ]; then
+  cd $R && DTA_TEST_LOG_DIR=$OUT timeout -k 10 840 python -u -m pytest tests/ -m gpu -v --timeout 240 --timeout-method thread > $OUT/tests.log 2>&1
+  rc=$?
+  grep -E "FAILED|ERROR" $OUT/tests.log | head -20
+  tail -2 $OUT/tests.log
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "TESTS_ABORTED rc=$rc"; exit 1; fi
+  timeout -k 10 400 python bench.py --cpu-baseline off > $OUT/bench.json 2> $OUT/bench.err || { echo BENCH_FAILED; tail -20 $OUT/bench.err; exit 1; }
+  python3 -c "
+import json; d=json.loads(open('$OUT/bench.json').read().strip().splitlines()[-1])
+print('value', d['value'], 'ms', d['ms_per_step'], {k: v['ms'] for k, v in d['kernels'].items()}, 'train', d.get('train', {}).get('value'), 'hbm', {k: v.get('GBps') for k, v in d.get('hbm_kernels', {}).items()})"
+fi
