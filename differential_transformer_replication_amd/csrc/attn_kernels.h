@@ -3679,21 +3679,29 @@ static inline int set_smem(K kernel, int bytes) {
 // B*T*H*dv elements).  One thread per 16 bytes of an output row, fp32 sums.
 // NC > 0: the branch count at compile time; 0: p.N at run time (branch counts without
 // an N-branch plan, which always run branch-split).
+// index split by launch-constant fast division (the int64 div / mod it replaced cost more
+// VALU than the kernel's HBM time); the output is written once by whole 16-byte vectors
+struct CombineDiv {
+  FastDiv vpr, H, T;
+};
+inline CombineDiv combine_div(const FwdParams& p, int esize) {
+  return CombineDiv{FastDiv((uint32_t)(p.DV / (16 / esize))), FastDiv((uint32_t)p.H), FastDiv((uint32_t)p.T)};
+}
 template <class E, int NC>
-__global__ __launch_bounds__(256) void branch_combine_kernel(FwdParams p) {
+__global__ __launch_bounds__(256) void branch_combine_kernel(FwdParams p, CombineDiv dv) {
   const int N = NC > 0 ? NC : p.N;
   constexpr int V = 16 / (int)sizeof(E);
   typedef float f32xv __attribute__((ext_vector_type(V)));
   typedef E ev __attribute__((ext_vector_type(V)));
-  const int vpr = p.DV / V;                                 // 16-byte vectors per (b, t, h) row
-  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t rows = (int64_t)p.B * p.T * p.H;
-  if (idx >= rows * vpr) return;
-  const int64_t row = idx / vpr;
-  const int e = (int)(idx - row * vpr) * V;
-  const int hh = (int)(row % p.H);
-  const int64_t bt = row / p.H;
-  const int t = (int)(bt % p.T), b = (int)(bt / p.T);
+  const uint32_t idx = blockIdx.x * 256 + threadIdx.x;
+  const uint32_t total = (uint32_t)p.B * p.T * p.H * dv.vpr.d;
+  if (idx >= total) return;
+  const uint32_t row = dv.vpr.div(idx);
+  const int e = (int)(idx - row * dv.vpr.d) * V;
+  const uint32_t bt = dv.H.div(row);
+  const int hh = (int)(row - bt * p.H);
+  const uint32_t b = dv.T.div(bt);
+  const int t = (int)(bt - b * p.T);
   const float* src = reinterpret_cast<const float*>(p.obr.p) + b * p.obr.sb + (int64_t)t * p.obr.st + hh * p.obr.sh + e;
   f32xv acc = f32xv{};
 #pragma unroll
@@ -3706,7 +3714,8 @@ __global__ __launch_bounds__(256) void branch_combine_kernel(FwdParams p) {
   ev y;
 #pragma unroll
   for (int j = 0; j < V; ++j) y[j] = (E)acc[j];
-  *reinterpret_cast<ev*>(reinterpret_cast<E*>(p.o.p) + b * p.o.sb + (int64_t)t * p.o.st + hh * p.o.sh + e) = y;
+  __builtin_nontemporal_store(y, reinterpret_cast<ev*>(reinterpret_cast<E*>(p.o.p) + b * p.o.sb + (int64_t)t * p.o.st +
+                                                       hh * p.o.sh + e));
 }
 
 // Branch-split forward policy: workgroups that hold ONE branch over the whole dv instead
@@ -3763,7 +3772,9 @@ int launch_fwd_t(const FwdParams& p, hipStream_t st) {
       q.bsplit = N;
       if (int e = launch_fwd_t<E, HS, 1, DV_, DROP>(q, st)) return e;
       const int64_t n = (int64_t)p.B * p.T * p.H * (PL::DV / (16 / (int)sizeof(E)));
-      hipLaunchKernelGGL((branch_combine_kernel<E, N>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, p);
+      if (n >= (1ll << 31)) return -2;
+      hipLaunchKernelGGL((branch_combine_kernel<E, N>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, p,
+                         combine_div(p, (int)sizeof(E)));
       return (int)hipGetLastError();
     }
   }
@@ -3981,7 +3992,9 @@ int fwd_branch_split_any(const FwdParams& p, hipStream_t st) {
 #undef DTA_F1
   if (e) return e;
   const int64_t n = (int64_t)p.B * p.T * p.H * (p.DV / (16 / (int)sizeof(E)));
-  hipLaunchKernelGGL((branch_combine_kernel<E, 0>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, p);
+  if (n >= (1ll << 31)) return -2;
+  hipLaunchKernelGGL((branch_combine_kernel<E, 0>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, p,
+                     combine_div(p, (int)sizeof(E)));
   return (int)hipGetLastError();
 }
 

@@ -238,4 +238,16 @@ __device__ __forceinline__ void store4_lds(E* dst, float a, float b, float c, fl
 
 constexpr float LOG2E = 1.4426950408889634f;
 
+// 32-bit division by a launch constant: q = (umulhi(x, m) + x) >> s, exact for x < 2^31
+// (round-up multiplier; the element index of a launch stays below 2^31 on this path)
+struct FastDiv {
+  uint32_t d, m, s;
+  FastDiv() = default;
+  explicit FastDiv(uint32_t d_) : d(d_), m(0), s(0) {
+    while ((1ull << s) < d) ++s;
+    m = (uint32_t)((((1ull << s) - d) << 32) / d + 1);
+  }
+  __device__ __forceinline__ uint32_t div(uint32_t x) const { return (__umulhi(x, m) + x) >> s; }
+};
+
 }  // namespace dta

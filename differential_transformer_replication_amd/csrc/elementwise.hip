@@ -440,17 +440,6 @@ __global__ __launch_bounds__(256) void ln_bwd_reduce2_kernel(const float* part2,
 }
 
 
-// 32-bit division by a launch constant: q = (umulhi(x, m) + x) >> s, exact for x < 2^31
-// (round-up multiplier; the element index of a launch stays below 2^31 on this path)
-struct FastDiv {
-  uint32_t d, m, s;
-  FastDiv() = default;
-  explicit FastDiv(uint32_t d_) : d(d_), m(0), s(0) {
-    while ((1ull << s) < d) ++s;
-    m = (uint32_t)((((1ull << s) - d) << 32) / d + 1);
-  }
-  __device__ __forceinline__ uint32_t div(uint32_t x) const { return (__umulhi(x, m) + x) >> s; }
-};
 struct RopeDiv { FastDiv row, T, per_row, N; uint32_t rowlen; };
 
 // one thread = 4 rotation pairs (8 elements); the 64-bit index decomposition of the first

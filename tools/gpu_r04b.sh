@@ -40,3 +40,15 @@ if [ -n "$FULL" ]; then
 import json; d=json.loads(open('$OUT/bench.json').read().strip().splitlines()[-1])
 print('value', d['value'], 'ms', d['ms_per_step'], {k: v['ms'] for k, v in d['kernels'].items()}, 'train', d.get('train', {}).get('value'), 'hbm', {k: v.get('GBps') for k, v in d.get('hbm_kernels', {}).items()})"
 fi
+if [ -n "$LNPROF" ]; then
+  mkdir -p $R/$OUT/lnprof; cd /tmp && export TMPDIR=/tmp
+  timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $R/$OUT/lnprof -o run -- python3 $R/tools/ab_ln.py base=lib/libdiffattn.so > $R/$OUT/lnprof/log.txt 2>&1 || { echo LNPROF_FAILED; tail -5 $R/$OUT/lnprof/log.txt; exit 1; }
+  cd $R; f=$(find $OUT/lnprof -name "*kernel_stats.csv" | head -1); [ -n "$f" ] && cut -d, -f1-8 $f | head -12
+fi
+if [ -n "$CFG3AB" ]; then
+  cd $R
+  for v in 0 1; do DTA_FWD3=$v timeout -k 10 200 python tools/ab_kernels.py base=lib/libdiffattn.so --shape 16,6,64,3,2048 --rounds 3 --reps 6 > $OUT/cfg3_fwd3_$v.json 2>/dev/null || { echo CFG3AB_FAILED; exit 1; }; done
+  python3 -c "
+import json
+for v in (0, 1): print('cfg3 N=3 DTA_FWD3', v, json.load(open('$OUT/cfg3_fwd3_%d.json' % v))['builds']['base']['median_ms'])"
+fi
