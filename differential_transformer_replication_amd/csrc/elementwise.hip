@@ -6,9 +6,11 @@
 //                      16-byte vector loads, two-pass mean/variance in registers.
 //  * rope              interleaved-pair rotary embedding of every Q_i / K_i and
 //                      its inverse for the gradients (Ndiff_transformer.py:11-22).
-//  * bwd_delta         delta_i[b,h,t] = <dO, O_i> per row (flash-bwd preprocess);
-//  * dcoef_reduce      dcoef[h][i] = sum_{b,t} delta_i  (d lambda, SURVEY semantic 5).
+//  * dcoef_reduce      dcoef[h][i] = sum of the dQ kernel's per-block partials of
+//                      delta_i = <dO, O_i>  (d lambda, SURVEY semantic 5), fixed order.
 //  * cast_f32          fp32 dQ accumulator -> activation dtype.
+//  * swiglu / accumulate / swiglu_bias   the training step's fused elementwise passes.
+// Every output is written once with non-temporal stores (DTA_EW_NT).
 #include <type_traits>
 
 #include "dta_common.h"
