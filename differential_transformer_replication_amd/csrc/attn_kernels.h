@@ -344,6 +344,56 @@ __device__ __forceinline__ void stage(E* img, const E* g, int64_t rs, int row0, 
   }
 }
 
+// RoPE at load (Ndiff_transformer.py:11-22, 104-109: interleaved pairs, rotation in fp32):
+// fr = fp32 [T][HS/2][2] (cos, sin).  rope_frag rotates one operand fragment of query row t
+// in registers (column col = the fragment's first k); rope_lds rotates ROWS staged rows of
+// an LDS image in place and, with `write`, stores the rotated rows to gout (row stride
+// ors) -- the copy the backward reads.
+template <class E>
+__device__ __forceinline__ void rope_frag(typename Ops<E>::frag& f, const float* fr, int t, int col, int HS, int hf) {
+  if constexpr (sizeof(E) == 2) {
+    const float* q = fr + ((int64_t)t * (HS / 2) + col / 2) * 2;
+    const f32x4 a = *reinterpret_cast<const f32x4*>(q), b = *reinterpret_cast<const f32x4*>(q + 4);
+    const float cs[4] = {a[0], a[2], b[0], b[2]}, sn[4] = {a[1], a[3], b[1], b[3]};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float x = (float)f[2 * j], y = (float)f[2 * j + 1];
+      f[2 * j] = (E)(x * cs[j] - y * sn[j]);
+      f[2 * j + 1] = (E)(x * sn[j] + y * cs[j]);
+    }
+  } else {
+    // fp32 fragments: k = 2s + hf, so a pair's two elements sit in lanes l and l ^ 32
+    const float* q = fr + ((int64_t)t * (HS / 2) + col / 2) * 2;
+    const float c = q[0], sn = q[1];
+    const float other = __shfl_xor(f, 32, 64);
+    f = hf == 0 ? f * c - other * sn : other * sn + f * c;
+  }
+}
+template <class E, int COLS, int ROWS, int VALID, int NTHR>
+__device__ __forceinline__ void rope_lds(E* img, const float* fr, int row0, int T, E* gout, int64_t ors, bool write,
+                                         int tid) {
+  using I = Img<E, COLS>;
+  constexpr int V = 16 / (int)sizeof(E);
+  typedef E vec __attribute__((ext_vector_type(V)));
+  for (int x = tid; x < ROWS * I::CPR; x += NTHR) {
+    const int r = x / I::CPR, ch = x % I::CPR;
+    if (ch * V >= VALID) continue;
+    const int t = min(row0 + r, T - 1);
+    vec* a = reinterpret_cast<vec*>(reinterpret_cast<char*>(img) + r * I::ROWB + ((ch ^ swz<I::ROWB>(r)) << 4));
+    vec v = *a;
+    const float* q = fr + ((int64_t)t * (VALID / 2) + ch * V / 2) * 2;
+#pragma unroll
+    for (int j = 0; j < V / 2; ++j) {
+      const float c = q[2 * j], sn = q[2 * j + 1];
+      const float xx = (float)v[2 * j], yy = (float)v[2 * j + 1];
+      v[2 * j] = (E)(xx * c - yy * sn);
+      v[2 * j + 1] = (E)(xx * sn + yy * c);
+    }
+    *a = v;
+    if (write && row0 + r < T) *reinterpret_cast<vec*>(gout + (int64_t)(row0 + r) * ors + ch * V) = v;
+  }
+}
+
 // Multiply n elements of an LDS array by s in place (16 bytes per lane and step; n
 // a multiple of 16 / sizeof(E)).  Every thread of the block calls it between barriers.
 template <class E, int NTHR>
@@ -707,6 +757,23 @@ void attn_fwd_kernel(FwdParams p) {
 #pragma unroll
   for (int i = NQR; i < N; ++i)
     stage<E, HSP, BM, HS, NTHR>(Qs + (i - NQR) * BM * HSP, gq + i * p.q.si, p.q.st, q0, T - 1, tid);
+  // RoPE at load (p.rope, ABI 5): Q_i arrive un-rotated; the rows in registers turn here,
+  // the LDS-staged ones once they land (first attempt); each rotated row is stored once to
+  // p.qrot for the backward (by the dv chunk 0 workgroup), so the RoPE pass rotates K only
+  const bool qrope = p.rope != nullptr;
+  E* gqr = qrope ? reinterpret_cast<E*>(p.qrot.p) + b * p.qrot.sb + hh * p.qrot.sh + br * p.qrot.si : nullptr;
+  bool qrot_pending = qrope && N > NQR;
+  if (qrope) {
+    const int tr = min(qrow, T - 1);
+#pragma unroll
+    for (int i = 0; i < NQR; ++i)
+#pragma unroll
+      for (int s = 0; s < NSQ; ++s) {
+        rope_frag<E>(qf[i][s], p.rope, tr, s * KS + hf * O::KH, HS, hf);
+        if (dc0 == 0 && qrow < T)
+          *reinterpret_cast<frag*>(gqr + (int64_t)qrow * p.qrot.st + i * p.qrot.si + s * KS + hf * O::KH) = qf[i][s];
+      }
+  }
 
   const int kend = min(T, q0 + BM);
   const int ntiles = (kend + BN - 1) / BN;
@@ -999,6 +1066,14 @@ void attn_fwd_kernel(FwdParams p) {
       if (j < ntiles) stage_kv(j, j);
     wait_vm(tile_pieces * max(0, min(NS - 1, ntiles) - 1));   // tile 0 (and the Q block) landed
     lds_barrier();
+    if (qrot_pending) {
+#pragma unroll
+      for (int i = NQR; i < N; ++i)
+        rope_lds<E, HSP, BM, HS, NTHR>(Qs + (i - NQR) * BM * HSP, p.rope, q0, T, gqr + i * p.qrot.si, p.qrot.st,
+                                       dc0 == 0, tid);
+      lds_barrier();
+      qrot_pending = false;
+    }
 #pragma unroll
     for (int i = 0; i < N; ++i) {
       m[i] = -INFINITY;
@@ -3783,7 +3858,7 @@ int launch_fwd_t(const FwdParams& p, hipStream_t st) {
   } else {
   if constexpr (Fw3Cfg<E, HS, N, PL::DV>::ok && !DROP) {
     // one wave per SIMD, key tiles software-pipelined (attn_fwd3_kernel, unit attn_bf16_dq2.hip)
-    if (kv_layout_ok(p, (int)sizeof(E)) && fwd3_env()) {
+    if (!p.rope && kv_layout_ok(p, (int)sizeof(E)) && fwd3_env()) {
       FwdParams q = p;
       q.N = N;            // a branch-split launch runs the N = 1 instance with p.N = the call's N
       return launch_attn_fwd3_bf16(q, st);
@@ -3791,7 +3866,7 @@ int launch_fwd_t(const FwdParams& p, hipStream_t st) {
   }
   if constexpr (Fw2Cfg<E, HS, N, PL::DV>::ok && !DROP) {
     // one wave per SIMD, two 32-row blocks per wave (attn_fwd2_kernel, unit attn_bf16_dq2.hip)
-    if (kv_layout_ok(p, (int)sizeof(E)) && fwd2_env()) return launch_attn_fwd2_bf16(p, st);
+    if (!p.rope && kv_layout_ok(p, (int)sizeof(E)) && fwd2_env()) return launch_attn_fwd2_bf16(p, st);
   }
   const int nsp = (N == 1 && p.bsplit > 1) ? p.bsplit : 1;
   dim3 grid((p.T + NW * 32 - 1) / (NW * 32), p.H * nsp * (PL::DV / DVC), p.B);

@@ -198,6 +198,11 @@ int dta_attn_fwd(const dta_attn_fwd_args* a, void* stream) {
   p.B = a->B; p.T = a->T; p.H = a->H; p.N = a->n_terms; p.HS = a->head_size; p.DV = a->dv;
   p.sl2 = a->scale * kLog2e;
   p.cst = a->n_terms;
+  if (a->rope_freqs) {
+    if (a->head_size % 2 || ((uintptr_t)a->rope_freqs & 15) || !ok_tensor(a->q_rot, a->dtype, true)) return DTA_ERR_INVALID;
+    p.rope = a->rope_freqs;
+    p.qrot = t5(a->q_rot);
+  }
   p.stamps = stamp_buf();
   return status(launch_attn_fwd(a->dtype, p, (hipStream_t)stream));
 }

@@ -24,6 +24,8 @@ struct FwdParams {
   int bsplit;          // launcher-internal: > 1 = branch-split launch of the N = 1 kernel
                        // (one branch of bsplit per workgroup; writes O_i and LSE_i only)
   int cst;             // row stride of coef [h][cst] (the call's total branch count)
+  const float* rope;   // if set (ABI 5): q is un-rotated; the forward rotates Q_i at load
+  T5 qrot;             //   (fp32 [T][HS/2][2] table) and stores the rotated rows here
 };
 
 struct BwdParams {

@@ -130,21 +130,25 @@ class _DiffAttention(torch.autograd.Function):
         stream = _lib.stream_handle(dev)
         q, k, v = split_packed(qkv, H, N, hs, dv)
         qk_rot = None
+        rope_args = (None, _lib.DtaTensor())
         if freqs is not None:
-            # RoPE of every Q_i/K_i (Ndiff_transformer.py:104-109): [Q|K] viewed as 2H heads
+            # RoPE of every Q_i/K_i (Ndiff_transformer.py:104-109): the K_i by one rotation pass,
+            # the Q_i inside the forward kernel as it loads them (it also stores the rotated
+            # rows into qk_rot for the backward)
             qk_rot = torch.empty(B, T, 2 * H, N, hs, device=dev, dtype=qkv.dtype)
-            src = qkv[..., :2 * H * N * hs].unflatten(-1, (2 * H, N, hs))
-            ra = _lib.RopeArgs(dt, B, T, 2 * H, N, hs, 0, 0, _lib.tensor5(src), _lib.tensor5(qk_rot),
+            src = k
+            ra = _lib.RopeArgs(dt, B, T, H, N, hs, 0, 0, _lib.tensor5(src), _lib.tensor5(qk_rot[:, :, H:]),
                                freqs.data_ptr())
             _lib.check(lib.dta_rope(ra, stream))
-            q, k = qk_rot[:, :, :H], qk_rot[:, :, H:]
+            k = qk_rot[:, :, H:]
+            rope_args = (freqs.data_ptr(), _lib.tensor5(qk_rot[:, :, :H]))
         o = torch.empty(B, T, H, dv, device=dev, dtype=qkv.dtype)
         obr = torch.empty(N, B, T, H, dv, device=dev, dtype=torch.float32)   # fp32 O_i (delta_i, d(coef))
         lse = torch.empty(N, B, H, T, device=dev, dtype=torch.float32)
         obr_t = _lib.DtaTensor(obr.data_ptr(), *obr.stride()[1:4], obr.stride(0))
         a = _lib.AttnFwdArgs(dt, B, T, H, N, hs, dv, scale, dropout_p,
                              _lib.tensor5(q), _lib.tensor5(k), _lib.tensor5(v), _lib.tensor5(o), obr_t,
-                             lse.data_ptr(), coef.data_ptr(), seed)
+                             lse.data_ptr(), coef.data_ptr(), seed, *rope_args)
         with TIMER.region("attn_fwd"):
             _lib.check(lib.dta_attn_fwd(a, stream))
         ctx.save_for_backward(qkv, qk_rot, obr, lse, coef, freqs)

@@ -42,7 +42,8 @@
 extern "C" {
 #endif
 
-#define DTA_ABI_VERSION 4   /* 4: Obr is fp32 for every dtype; any n_terms >= 1 */
+#define DTA_ABI_VERSION 5   /* 5: RoPE of Q_i at the forward's load (rope_freqs, q_rot);
+                               4: Obr is fp32 for every dtype; any n_terms >= 1 */
 
 enum dta_dtype { DTA_BF16 = 0, DTA_F16 = 1, DTA_F32 = 2 };
 
@@ -63,7 +64,7 @@ typedef struct dta_tensor {
  * Replaces, for all heads at once, DiffHead.forward's scores/mask/softmax/
  * dropout/combine/@V (diff_transformer.py:57-72), the per-head loop
  * (diff_transformer.py:89) and AlternatingDiffHead's branch loop
- * (Ndiff_transformer.py:102-125; RoPE is applied beforehand by dta_rope).
+ * (Ndiff_transformer.py:102-125; RoPE: K_i beforehand by dta_rope, Q_i at load, rope_freqs).
  * O = sum_i coef[h][i] * softmax(mask(Q_i K_i^T / sqrt(hs))) V. */
 typedef struct dta_attn_fwd_args {
   int32_t dtype;             /* enum dta_dtype */
@@ -81,6 +82,13 @@ typedef struct dta_attn_fwd_args {
   float* lse;                /* output fp32 [i][b][h][t], contiguous */
   const float* coef;         /* fp32 [h][i], contiguous */
   uint64_t dropout_seed;     /* with dropout_p > 0: the mask's seed (pass the same to dta_attn_bwd) */
+  /* ABI 5, optional: RoPE of Q_i fused into the load (Ndiff_transformer.py:104-109).
+   * With rope_freqs (fp32 [T][head_size/2][2] (cos, sin), 16-byte aligned) q holds the
+   * UN-rotated Q_i; the kernel rotates each row as it loads it and writes the rotated row
+   * to q_rot (same shape as q, dtype) for dta_attn_bwd.  k must already be rotated
+   * (dta_rope over the K_i only).  NULL: q is used as given. */
+  const float* rope_freqs;
+  dta_tensor q_rot;
 } dta_attn_fwd_args;
 
 int dta_attn_fwd(const dta_attn_fwd_args* a, void* stream);
