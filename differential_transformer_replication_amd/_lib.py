@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get("DTA_LIB", os.path.join(_HERE, "lib", "libdiffattn.so"
 DTA_BF16, DTA_F16, DTA_F32 = 0, 1, 2
 _DTYPES = {torch.bfloat16: DTA_BF16, torch.float16: DTA_F16, torch.float32: DTA_F32}
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 # every symbol include/diffattn.h declares
 EXPORTS = ("dta_attn_fwd", "dta_attn_bwd", "dta_attn_bwd_workspace_bytes", "dta_attn_bwd_dcoef_partial_bytes",
@@ -51,7 +51,8 @@ class AttnFwdArgs(ctypes.Structure):
                 ("dv", ctypes.c_int32), ("scale", ctypes.c_float), ("dropout_p", ctypes.c_float),
                 ("q", DtaTensor), ("k", DtaTensor), ("v", DtaTensor), ("o", DtaTensor),
                 ("obr", DtaTensor), ("lse", ctypes.c_void_p), ("coef", ctypes.c_void_p),
-                ("dropout_seed", ctypes.c_uint64), ("rope_freqs", ctypes.c_void_p), ("q_rot", DtaTensor)]
+                ("dropout_seed", ctypes.c_uint64), ("rope_freqs", ctypes.c_void_p), ("q_rot", DtaTensor),
+                ("obr_dtype", ctypes.c_int32)]
 
 
 class AttnBwdArgs(ctypes.Structure):
@@ -63,7 +64,7 @@ class AttnBwdArgs(ctypes.Structure):
                 ("dq", DtaTensor), ("dk", DtaTensor), ("dv_out", DtaTensor),
                 ("dcoef", ctypes.c_void_p), ("delta", ctypes.c_void_p), ("dq_f32", ctypes.c_void_p),
                 ("stages", ctypes.c_int32), ("rope_freqs", ctypes.c_void_p), ("dcoef_partial", ctypes.c_void_p),
-                ("dropout_seed", ctypes.c_uint64)]
+                ("dropout_seed", ctypes.c_uint64), ("obr_dtype", ctypes.c_int32)]
 
 
 BWD_PRE, BWD_DQ, BWD_DKDV = 1, 2, 4

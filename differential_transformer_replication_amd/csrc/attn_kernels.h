@@ -1122,9 +1122,9 @@ void attn_fwd_kernel(FwdParams p) {
       p.lse[(((int64_t)(br + i) * p.B + b) * p.H + hh) * T + qrow] = -(m[i] + __builtin_log2f(lt));   // stored negated
   }
   E* go = reinterpret_cast<E*>(p.o.p) + b * p.o.sb + (int64_t)qrow * p.o.st + hh * p.o.sh + dc0;
-  // O_i stays fp32 (saved for the backward's delta_i = <dO, O_i>, whose sums feed d(lambda))
-  float* gob = reinterpret_cast<float*>(p.obr.p) + b * p.obr.sb + (int64_t)qrow * p.obr.st + hh * p.obr.sh +
-               br * p.obr.si + dc0;
+  // O_i saved for the backward's delta_i = <dO, O_i> (whose sums feed d(lambda)): fp32, or
+  // fp16 (p.ob16: 2^-11, eight times bf16's resolution, half the bytes)
+  const int64_t gob = b * p.obr.sb + (int64_t)qrow * p.obr.st + hh * p.obr.sh + br * p.obr.si + dc0;
 #pragma unroll
   for (int d = 0; d < NDB; ++d)
 #pragma unroll
@@ -1135,7 +1135,7 @@ void attn_fwd_kernel(FwdParams p) {
       for (int i = 0; i < N; ++i) {
         const float a0 = acc[i][d][4 * g + 0] * inv[i], a1 = acc[i][d][4 * g + 1] * inv[i];
         const float a2 = acc[i][d][4 * g + 2] * inv[i], a3 = acc[i][d][4 * g + 3] * inv[i];
-        store4<float>(gob + i * p.obr.si + e, a0, a1, a2, a3);
+        store_ob4(p.obr.p, gob + i * p.obr.si + e, p.ob16, a0, a1, a2, a3);
         o0 = fmaf(coef[i], a0, o0); o1 = fmaf(coef[i], a1, o1);
         o2 = fmaf(coef[i], a2, o2); o3 = fmaf(coef[i], a3, o3);
       }
@@ -1220,7 +1220,7 @@ void attn_dq_kernel(BwdParams p) {
   const E* gk = reinterpret_cast<const E*>(p.k.p) + b * p.k.sb + hh * p.k.sh;
   const E* gv = reinterpret_cast<const E*>(p.v.p) + b * p.v.sb + hh * p.v.sh;
   const E* gdo = reinterpret_cast<const E*>(p.dout.p) + b * p.dout.sb + hh * p.dout.sh;
-  const float* gob = reinterpret_cast<const float*>(p.obr.p) + b * p.obr.sb + hh * p.obr.sh;   // fp32 O_i
+  const int64_t gob = b * p.obr.sb + hh * p.obr.sh;   // O_i: fp32, or fp16 with p.ob16
 
   const int kend = min(T, q0 + BM);
   const int ntiles = (kend + BN - 1) / BN;
@@ -1274,15 +1274,14 @@ void attn_dq_kernel(BwdParams p) {
     if (rowok) {
 #pragma unroll
       for (int s = 0; s < NSV; ++s) {
-        const float* o = gob + (int64_t)qrow * p.obr.st + i * p.obr.si + s * KS + hf * O::KH;
+        const int64_t o = gob + (int64_t)qrow * p.obr.st + i * p.obr.si + s * KS + hf * O::KH;
         if constexpr (sizeof(E) == 2) {
-          const f32x4 o0 = *reinterpret_cast<const f32x4*>(o), o1 = *reinterpret_cast<const f32x4*>(o + 4);
+          float ov[8];
+          load_ob8(p.obr.p, o, p.ob16, ov);
 #pragma unroll
-          for (int j = 0; j < 4; ++j) d = fmaf((float)df[s][j], o0[j], d);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) d = fmaf((float)df[s][4 + j], o1[j], d);
+          for (int j = 0; j < 8; ++j) d = fmaf((float)df[s][j], ov[j], d);
         } else {
-          d = fmaf(df[s], *o, d);
+          d = fmaf(df[s], reinterpret_cast<const float*>(p.obr.p)[o], d);
         }
       }
     }
@@ -1770,7 +1769,7 @@ void attn_dq2_kernel(BwdParams p) {
   const E* gk = reinterpret_cast<const E*>(p.k.p) + b * p.k.sb + hh * p.k.sh;
   const E* gv = reinterpret_cast<const E*>(p.v.p) + b * p.v.sb + hh * p.v.sh;
   const E* gdo = reinterpret_cast<const E*>(p.dout.p) + b * p.dout.sb + hh * p.dout.sh;
-  const float* gob = reinterpret_cast<const float*>(p.obr.p) + b * p.obr.sb + hh * p.obr.sh;
+  const int64_t gob = b * p.obr.sb + hh * p.obr.sh;
   const int kend = min(T, q0 + BM);
   const int ntiles = (kend + BN - 1) / BN;
   using KR = KvRing<E, HS, N, DV, BN, NW>;
@@ -1806,12 +1805,10 @@ void attn_dq2_kernel(BwdParams p) {
       if (rowok) {
 #pragma unroll
         for (int s = 0; s < NSV; ++s) {
-          const float* o = gob + (int64_t)qrow * p.obr.st + i * p.obr.si + s * KS + hf * O::KH;
-          const f32x4 o0 = *reinterpret_cast<const f32x4*>(o), o1 = *reinterpret_cast<const f32x4*>(o + 4);
+          float ov[8];
+          load_ob8(p.obr.p, gob + (int64_t)qrow * p.obr.st + i * p.obr.si + s * KS + hf * O::KH, p.ob16, ov);
 #pragma unroll
-          for (int j = 0; j < 4; ++j) d = fmaf((float)df[qb][s][j], o0[j], d);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) d = fmaf((float)df[qb][s][4 + j], o1[j], d);
+          for (int j = 0; j < 8; ++j) d = fmaf((float)df[qb][s][j], ov[j], d);
         }
       }
       d = wave_sum_halves(d);
@@ -2907,7 +2904,7 @@ void attn_fwd2_kernel(FwdParams p) {
       if (hf == 0) p.lse[(((int64_t)i * p.B + b) * p.H + hh) * T + qrow] = -(m[u] + __builtin_log2f(lt));
     }
     E* go = reinterpret_cast<E*>(p.o.p) + b * p.o.sb + (int64_t)qrow * p.o.st + hh * p.o.sh;
-    float* gob = reinterpret_cast<float*>(p.obr.p) + b * p.obr.sb + (int64_t)qrow * p.obr.st + hh * p.obr.sh;
+    const int64_t gob = b * p.obr.sb + (int64_t)qrow * p.obr.st + hh * p.obr.sh;
 #pragma unroll
     for (int d = 0; d < NDB; ++d)
 #pragma unroll
@@ -2919,7 +2916,7 @@ void attn_fwd2_kernel(FwdParams p) {
           const int u = 2 * i + qb;
           const float a0 = acc[u][d][4 * g + 0] * inv[i], a1 = acc[u][d][4 * g + 1] * inv[i];
           const float a2 = acc[u][d][4 * g + 2] * inv[i], a3 = acc[u][d][4 * g + 3] * inv[i];
-          store4<float>(gob + i * p.obr.si + e, a0, a1, a2, a3);
+          store_ob4(p.obr.p, gob + i * p.obr.si + e, p.ob16, a0, a1, a2, a3);
           const float c = p.coef[hh * p.cst + i];
           o0 = fmaf(c, a0, o0); o1 = fmaf(c, a1, o1); o2 = fmaf(c, a2, o2); o3 = fmaf(c, a3, o3);
         }
@@ -3351,7 +3348,7 @@ void attn_fwd3_kernel(FwdParams p) {
     if (hf == 0) p.lse[(((int64_t)(br + i) * p.B + b) * p.H + hh) * T + qrow] = -(m[i] + __builtin_log2f(lt));
   }
   E* go = reinterpret_cast<E*>(p.o.p) + b * p.o.sb + (int64_t)qrow * p.o.st + hh * p.o.sh;
-  float* gob = reinterpret_cast<float*>(p.obr.p) + b * p.obr.sb + (int64_t)qrow * p.obr.st + hh * p.obr.sh + br * p.obr.si;
+  const int64_t gob = b * p.obr.sb + (int64_t)qrow * p.obr.st + hh * p.obr.sh + br * p.obr.si;
 #pragma unroll
   for (int d = 0; d < NDB; ++d)
 #pragma unroll
@@ -3362,7 +3359,7 @@ void attn_fwd3_kernel(FwdParams p) {
       for (int i = 0; i < N; ++i) {
         const float a0 = acc[i][d][4 * g + 0] * inv[i], a1 = acc[i][d][4 * g + 1] * inv[i];
         const float a2 = acc[i][d][4 * g + 2] * inv[i], a3 = acc[i][d][4 * g + 3] * inv[i];
-        store4<float>(gob + i * p.obr.si + e, a0, a1, a2, a3);
+        store_ob4(p.obr.p, gob + i * p.obr.si + e, p.ob16, a0, a1, a2, a3);
         const float c = nsp > 1 ? 1.f : p.coef[hh * p.cst + i];
         o0 = fmaf(c, a0, o0); o1 = fmaf(c, a1, o1); o2 = fmaf(c, a2, o2); o3 = fmaf(c, a3, o3);
       }
@@ -3777,12 +3774,21 @@ __global__ __launch_bounds__(256) void branch_combine_kernel(FwdParams p, Combin
   const int hh = (int)(row - bt * p.H);
   const uint32_t b = dv.T.div(bt);
   const int t = (int)(bt - b * p.T);
-  const float* src = reinterpret_cast<const float*>(p.obr.p) + b * p.obr.sb + (int64_t)t * p.obr.st + hh * p.obr.sh + e;
+  const int64_t src = b * p.obr.sb + (int64_t)t * p.obr.st + hh * p.obr.sh + e;
   f32xv acc = f32xv{};
 #pragma unroll
   for (int i = 0; i < N; ++i) {
-    const f32xv x = *reinterpret_cast<const f32xv*>(src + i * p.obr.si);     // fp32 O_i
     const float c = p.coef[hh * p.cst + i];
+    if constexpr (V == 8) {
+      if (p.ob16) {                                                          // fp16 O_i
+        float x[8];
+        load_ob8(p.obr.p, src + i * p.obr.si, true, x);
+#pragma unroll
+        for (int j = 0; j < V; ++j) acc[j] = fmaf(c, x[j], acc[j]);
+        continue;
+      }
+    }
+    const f32xv x = *reinterpret_cast<const f32xv*>(reinterpret_cast<const float*>(p.obr.p) + src + i * p.obr.si);
 #pragma unroll
     for (int j = 0; j < V; ++j) acc[j] = fmaf(c, x[j], acc[j]);
   }

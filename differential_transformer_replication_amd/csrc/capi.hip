@@ -125,6 +125,12 @@ bool ok_tensor(const dta_tensor& t, int dtype, bool with_i) {
 
 T5 t5(const dta_tensor& t) { return T5{t.ptr, t.sb, t.st, t.sh, t.si}; }
 
+// obr (the per-branch O_i): fp32 (obr_dtype 0 or DTA_F32), or fp16 with 16-bit activations
+bool ok_obr(const dta_tensor& t, int obr_dtype, int dtype) {
+  if (obr_dtype == DTA_F16) return dtype != DTA_F32 && ok_tensor(t, DTA_F16, true);
+  return (obr_dtype == 0 || obr_dtype == DTA_F32) && ok_tensor(t, DTA_F32, true);
+}
+
 int status(int e) {
   if (e == 0) return DTA_OK;
   if (e == -2) return DTA_ERR_UNSUPPORTED;
@@ -191,8 +197,9 @@ int dta_attn_fwd(const dta_attn_fwd_args* a, void* stream) {
   if (!attn_supported(a->dtype, a->head_size, a->n_terms, a->dv)) return DTA_ERR_UNSUPPORTED;
   if ((int64_t)a->B * a->T == 0) return DTA_OK;
   if (!ok_tensor(a->q, a->dtype, true) || !ok_tensor(a->k, a->dtype, true) || !ok_tensor(a->v, a->dtype, false) ||
-      !ok_tensor(a->o, a->dtype, false) || !ok_tensor(a->obr, DTA_F32, true) || !a->lse || !a->coef)
+      !ok_tensor(a->o, a->dtype, false) || !ok_obr(a->obr, a->obr_dtype, a->dtype) || !a->lse || !a->coef)
     return DTA_ERR_INVALID;
+  p.ob16 = a->obr_dtype == DTA_F16;
   p.q = t5(a->q); p.k = t5(a->k); p.v = t5(a->v); p.o = t5(a->o); p.obr = t5(a->obr);
   p.lse = a->lse; p.coef = a->coef;
   p.B = a->B; p.T = a->T; p.H = a->H; p.N = a->n_terms; p.HS = a->head_size; p.DV = a->dv;
@@ -232,12 +239,13 @@ int dta_attn_bwd(const dta_attn_bwd_args* a, void* stream) {
   }
   if ((int64_t)a->B * a->T == 0) return DTA_OK;
   if (!ok_tensor(a->q, a->dtype, true) || !ok_tensor(a->k, a->dtype, true) || !ok_tensor(a->v, a->dtype, false) ||
-      !ok_tensor(a->obr, DTA_F32, true) || !ok_tensor(a->dout, a->dtype, false) ||
+      !ok_obr(a->obr, a->obr_dtype, a->dtype) || !ok_tensor(a->dout, a->dtype, false) ||
       !ok_tensor(a->dk, a->dtype, true) || !ok_tensor(a->dv_out, a->dtype, false) ||
       !a->lse || !a->coef || !a->delta)
     return DTA_ERR_INVALID;
   if (a->dq.ptr ? !ok_tensor(a->dq, a->dtype, true) : !aligned_ptr(a->dq_f32)) return DTA_ERR_INVALID;
   p.q = t5(a->q); p.k = t5(a->k); p.v = t5(a->v); p.obr = t5(a->obr); p.dout = t5(a->dout);
+  p.ob16 = a->obr_dtype == DTA_F16;
   p.dq = t5(a->dq); p.dk = t5(a->dk); p.dv = t5(a->dv_out);
   p.lse = a->lse; p.delta = a->delta; p.coef = a->coef; p.dcoef = a->dcoef;
   p.dq32 = a->dq.ptr ? nullptr : a->dq_f32;
@@ -258,7 +266,7 @@ int dta_attn_bwd(const dta_attn_bwd_args* a, void* stream) {
     BwdParams q = p;
     auto off = [&](T5& t) { t.p = (char*)t.p + (int64_t)g0 * t.si * es; };
     off(q.q); off(q.k); off(q.dk);
-    q.obr.p = (char*)q.obr.p + (int64_t)g0 * q.obr.si * 4;        // fp32
+    q.obr.p = (char*)q.obr.p + (int64_t)g0 * q.obr.si * (p.ob16 ? 2 : 4);
     if (q.dq.p) off(q.dq);
     if (q.dq32) q.dq32 += (int64_t)g0 * p.HS;
     q.lse += g0 * rowvec; q.delta += g0 * rowvec; q.coef += g0; q.dcoef += g0;

@@ -225,6 +225,25 @@ __device__ __forceinline__ void store4(E* dst, float a, float b, float c, float 
   }
 }
 
+// O_i (obr) elements: fp32, or fp16 (ABI 6, `h`) -- element offsets from the base
+__device__ __forceinline__ void store_ob4(void* base, int64_t off, bool h, float a, float b, float c, float d) {
+  if (h) store4<_Float16>(reinterpret_cast<_Float16*>(base) + off, a, b, c, d);
+  else store4<float>(reinterpret_cast<float*>(base) + off, a, b, c, d);
+}
+__device__ __forceinline__ void load_ob8(const void* base, int64_t off, bool h, float (&o)[8]) {
+  if (h) {
+    typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+    const h8 v = *reinterpret_cast<const h8*>(reinterpret_cast<const _Float16*>(base) + off);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (float)v[j];
+  } else {
+    const f32x4 a = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(base) + off);
+    const f32x4 b = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(base) + off + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { o[j] = a[j]; o[4 + j] = b[j]; }
+  }
+}
+
 template <class E>
 __device__ __forceinline__ void store4_lds(E* dst, float a, float b, float c, float d) {
   if constexpr (sizeof(E) == 2) {

@@ -26,6 +26,7 @@ struct FwdParams {
   int cst;             // row stride of coef [h][cst] (the call's total branch count)
   const float* rope;   // if set (ABI 5): q is un-rotated; the forward rotates Q_i at load
   T5 qrot;             //   (fp32 [T][HS/2][2] table) and stores the rotated rows here
+  int ob16;            // O_i (obr) stored as fp16 instead of fp32 (ABI 6, 16-bit activations)
 };
 
 struct BwdParams {
@@ -50,6 +51,7 @@ struct BwdParams {
                        // [h][cst], of the d(coef) partials and of dq32; dropout's branch index
   int br0;             // the group's first branch (dropout mask key)
   int dv_acc;          // dK/dV kernel: add into dv instead of storing (groups after the first)
+  int ob16;            // obr holds fp16 O_i (ABI 6)
 };
 
 // per-dtype launchers (dtype index: 0 bf16, 1 f16, 2 f32); return hipError_t

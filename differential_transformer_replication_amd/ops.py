@@ -110,6 +110,17 @@ def split_packed(qkv: Tensor, H: int, N: int, hs: int, dv: int):
     return q, k, v
 
 
+def _obr_dtype(dtype: torch.dtype) -> torch.dtype:
+    """Storage type of the saved per-branch outputs O_i (ABI 6 obr_dtype): fp32.  fp16 O_i
+    (DTA_OBR_F16=1, 16-bit activations) measured 0.7% off the cfg2 step but left one head's
+    d(lambda) at 1.22 relative error in the default-config bf16 model, against a bar of 0.56
+    (2x the reference algorithm's own bf16 error; fp32 O_i passes): the cancellation in
+    sum_rows delta_i needs O_i unrounded."""
+    if dtype != torch.float32 and os.environ.get("DTA_OBR_F16", "0") == "1":
+        return torch.float16
+    return torch.float32
+
+
 class _DiffAttention(torch.autograd.Function):
     @staticmethod
     def forward(ctx, qkv: Tensor, coef: Tensor, H: int, N: int, hs: int, freqs: Optional[Tensor], dv: int,
@@ -143,12 +154,13 @@ class _DiffAttention(torch.autograd.Function):
             k = qk_rot[:, :, H:]
             rope_args = (freqs.data_ptr(), _lib.tensor5(qk_rot[:, :, :H]))
         o = torch.empty(B, T, H, dv, device=dev, dtype=qkv.dtype)
-        obr = torch.empty(N, B, T, H, dv, device=dev, dtype=torch.float32)   # fp32 O_i (delta_i, d(coef))
+        # the per-branch O_i for delta_i = <dO, O_i> (hence d(coef), d(lambda)), fp32
+        obr = torch.empty(N, B, T, H, dv, device=dev, dtype=_obr_dtype(qkv.dtype))
         lse = torch.empty(N, B, H, T, device=dev, dtype=torch.float32)
         obr_t = _lib.DtaTensor(obr.data_ptr(), *obr.stride()[1:4], obr.stride(0))
         a = _lib.AttnFwdArgs(dt, B, T, H, N, hs, dv, scale, dropout_p,
                              _lib.tensor5(q), _lib.tensor5(k), _lib.tensor5(v), _lib.tensor5(o), obr_t,
-                             lse.data_ptr(), coef.data_ptr(), seed, *rope_args)
+                             lse.data_ptr(), coef.data_ptr(), seed, *rope_args, _lib.dtype_code(obr.dtype))
         with TIMER.region("attn_fwd"):
             _lib.check(lib.dta_attn_fwd(a, stream))
         ctx.save_for_backward(qkv, qk_rot, obr, lse, coef, freqs)
@@ -183,7 +195,8 @@ class _DiffAttention(torch.autograd.Function):
                              lse.data_ptr(), coef.data_ptr(), _lib.tensor5(do),
                              _lib.tensor5(dq), _lib.tensor5(dk), _lib.tensor5(dvv),
                              dcoef.data_ptr(), delta.data_ptr(), None, _lib.BWD_PRE,
-                             freqs.data_ptr() if freqs is not None else None, dcp.data_ptr(), ctx.drop[1])
+                             freqs.data_ptr() if freqs is not None else None, dcp.data_ptr(), ctx.drop[1],
+                             _lib.dtype_code(obr.dtype))
         _lib.check(lib.dta_attn_bwd(a, stream))
         a.stages = _lib.BWD_DQ
         with TIMER.region("attn_bwd_dq"):

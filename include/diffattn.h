@@ -42,7 +42,8 @@
 extern "C" {
 #endif
 
-#define DTA_ABI_VERSION 5   /* 5: RoPE of Q_i at the forward's load (rope_freqs, q_rot);
+#define DTA_ABI_VERSION 6   /* 6: obr_dtype (fp16 O_i for 16-bit activations);
+                               5: RoPE of Q_i at the forward's load (rope_freqs, q_rot);
                                4: Obr is fp32 for every dtype; any n_terms >= 1 */
 
 enum dta_dtype { DTA_BF16 = 0, DTA_F16 = 1, DTA_F32 = 2 };
@@ -78,7 +79,7 @@ typedef struct dta_attn_fwd_args {
                                 the row sums normalising the map see every element */
   dta_tensor q, k, v;        /* inputs */
   dta_tensor o;              /* output, combined */
-  dta_tensor obr;            /* output [i][b][t][h][e]: sb,st,sh,si = strides of b,t,h,i */
+  dta_tensor obr;            /* output [i][b][t][h][e]: sb,st,sh,si = strides of b,t,h,i; fp32 or fp16 (obr_dtype) */
   float* lse;                /* output fp32 [i][b][h][t], contiguous */
   const float* coef;         /* fp32 [h][i], contiguous */
   uint64_t dropout_seed;     /* with dropout_p > 0: the mask's seed (pass the same to dta_attn_bwd) */
@@ -89,6 +90,8 @@ typedef struct dta_attn_fwd_args {
    * (dta_rope over the K_i only).  NULL: q is used as given. */
   const float* rope_freqs;
   dta_tensor q_rot;
+  int32_t obr_dtype;         /* ABI 6: 0 / DTA_F32 = obr is fp32; DTA_F16 = fp16 (16-bit dtype only:
+                                2^-11 resolution, eight times bf16's, half the bytes of fp32) */
 } dta_attn_fwd_args;
 
 int dta_attn_fwd(const dta_attn_fwd_args* a, void* stream);
@@ -134,6 +137,7 @@ typedef struct dta_attn_bwd_args {
                                 order (bitwise reproducible run to run); without it the
                                 query-major kernel adds into dcoef by float atomics */
   uint64_t dropout_seed;     /* the forward's dropout seed */
+  int32_t obr_dtype;         /* ABI 6: as dta_attn_fwd_args (the forward's obr) */
 } dta_attn_bwd_args;
 
 enum { DTA_BWD_PRE = 1, DTA_BWD_DQ = 2, DTA_BWD_DKDV = 4 };

@@ -40,6 +40,7 @@ def main():
     ap.add_argument("--shape", default="8,16,64,2,4096")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--obr", choices=["f32", "f16"], default="f32", help="O_i storage (ABI 6 obr_dtype)")
     args = ap.parse_args()
     B, H, hs, N, T = (int(x) for x in args.shape.split(","))
     dv = 2 * hs
@@ -63,7 +64,7 @@ def main():
 
     def bufs():
         o = torch.empty(B, T, H, dv, device=dev, dtype=torch.bfloat16)
-        obr = torch.empty(N, B, T, H, dv, device=dev, dtype=torch.float32)
+        obr = torch.empty(N, B, T, H, dv, device=dev, dtype=torch.float16 if args.obr == "f16" else torch.float32)
         lse = torch.empty(N, B, H, T, device=dev)
         dqkv = torch.zeros_like(qkv)
         dcoef = torch.empty(H, N, device=dev)
@@ -76,6 +77,7 @@ def main():
         obr_t = _lib.DtaTensor(obr.data_ptr(), *obr.stride()[1:4], obr.stride(0))
         fa = _lib.AttnFwdArgs(0, B, T, H, N, hs, dv, scale, 0.0, _lib.tensor5(q), _lib.tensor5(k), _lib.tensor5(v),
                               _lib.tensor5(o), obr_t, lse.data_ptr(), coef.data_ptr())
+        fa.obr_dtype = 1 if args.obr == "f16" else 0
         dq = dqkv[..., :nq].unflatten(-1, (H, N, hs))
         dk = dqkv[..., nq:2 * nq].unflatten(-1, (H, N, hs))
         dvv = dqkv[..., 2 * nq:].unflatten(-1, (H, dv))
@@ -83,6 +85,7 @@ def main():
                               obr_t, lse.data_ptr(), coef.data_ptr(), _lib.tensor5(do), _lib.tensor5(dq),
                               _lib.tensor5(dk), _lib.tensor5(dvv), dcoef.data_ptr(), delta.data_ptr(), None,
                               _lib.BWD_PRE, None)
+        ba.obr_dtype = fa.obr_dtype
         state[name] = (lib, fa, ba, (o, obr, lse, dqkv, dcoef))
 
     def run(name, which):
