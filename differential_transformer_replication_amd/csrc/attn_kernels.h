@@ -2498,433 +2498,6 @@ void attn_dkdv_kernel(BwdParams p) {
   }
 }
 
-// --------------------------------------- forward: two query blocks per wave ---
-// attn_fwd2_kernel: attn_fwd_kernel's fixed-reference-maximum (FAST) forward re-planned for
-// one wave per SIMD: a wave owns two 32-row query blocks (the workgroup's 4 waves 256 rows),
-// the O_i^T accumulators of both blocks (N * dv / 32 x 16 registers per block) in AGPRs
-// (mfma_agpr), Q_i of the workgroup in LDS, K_i / V tiles of 64 keys through the LDS-DMA
-// ring.  The first key tile sets each row's reference maximum (per-tile max, as attn_fwd);
-// every later tile is a compile-time MFMA stream -- per unit u = (block, branch) the S^T
-// chain and the O^T += V^T P^T product -- with each unit's exp / row-sum / pack VALU placed
-// into the slots of MFMAs that do not depend on it (Fw2Sched, as Dq2Sched).  A workgroup
-// whose tile partial sums leave [0, LSMAX] (a row maximum that grew past what the packed
-// operand type holds) re-runs: one pass of S^T over all its tiles for the exact row maxima,
-// then the same stream with those maxima (every P <= 1).
-namespace fw2 {
-enum : int { SC = 0, PV = 1 };
-struct Op { int kind = 0, u = 0, qb = 0, i = 0, a = 0, b = 0, c = 0; };
-constexpr int PIECES = 16;
-
-template <int N, int NSQ, int NDB>
-struct Sched {
-  static constexpr int NKB = 2, U = 2 * N, SR = 3, PR = 2;     // S^T sets, packed-P sets in flight
-  static constexpr int NS1 = NSQ * NKB, NP1 = NDB * NKB * 2;
-  static constexpr int NOPS = U * NS1 + U * NP1;
-  static constexpr int ui(int u) { return u / 2; }
-  static constexpr int uq(int u) { return u % 2; }
-  Op ops[NOPS];
-  int s0[U] = {}, s1[U] = {}, p0[U] = {};
-  int E[U] = {}, Dl[U] = {};
-  int npiece[NOPS] = {};
-  int pu[NOPS][PIECES] = {};
-  int nreads[NOPS] = {};
-  int rid[NOPS] = {}, qid[NOPS] = {}, tid[NOPS] = {};
-  bool ok = true;
-  constexpr void add_s(int& n, int u) {
-    s0[u] = n;
-    for (int st = 0; st < NSQ; ++st)
-      for (int kb = 0; kb < NKB; ++kb) {
-        ops[n].kind = SC; ops[n].u = u; ops[n].qb = uq(u); ops[n].i = ui(u); ops[n].a = st; ops[n].b = kb; ++n;
-      }
-    s1[u] = n - 1;
-  }
-  constexpr void add_p(int& n, int u) {
-    p0[u] = n;
-    for (int d = 0; d < NDB; ++d)
-      for (int kb = 0; kb < NKB; ++kb)
-        for (int ks = 0; ks < 2; ++ks) {
-          ops[n].kind = PV; ops[n].u = u; ops[n].qb = uq(u); ops[n].i = ui(u); ops[n].a = d; ops[n].b = kb; ops[n].c = ks; ++n;
-        }
-  }
-  constexpr Sched() {
-    int n = 0;
-    add_s(n, 0);
-    add_s(n, 1);
-    for (int u = 2; u < U; ++u) { add_s(n, u); add_p(n, u - 2); }
-    add_p(n, U - 2); add_p(n, U - 1);
-    if (n != NOPS) ok = false;
-    for (int u = 0; u < U; ++u) {
-      E[u] = s1[u] + 1;
-      if (u >= PR && p0[u - PR] + NP1 > E[u]) E[u] = p0[u - PR] + NP1;     // its packed-P set is free
-      Dl[u] = p0[u] - 1;
-      if (u + SR < U && s0[u + SR] < Dl[u]) Dl[u] = s0[u + SR];
-    }
-    int load[NOPS] = {};
-    for (int u = 0; u < U; ++u) {
-      int cap = 1;
-      for (;; ++cap) {
-        int room = 0;
-        for (int x = E[u]; x < Dl[u]; ++x) room += load[x] < cap ? cap - load[x] : 0;
-        if (room >= PIECES || cap >= PIECES) break;
-      }
-      int j = 0;
-      for (int x = E[u]; x < Dl[u] && j < PIECES; ++x)
-        while (load[x] < cap && j < PIECES) {
-          if (npiece[x] < PIECES) pu[x][npiece[x]++] = u * PIECES + j; else ok = false;
-          ++load[x];
-          ++j;
-        }
-      if (j < PIECES) ok = false;
-    }
-    int nb = 0, nq = 0, ntr = 0;
-    for (int s = 0; s < NOPS; ++s) {
-      const Op& o = ops[s];
-      if (o.kind == SC) {
-        rid[s] = nb++; nreads[s] = 1;
-        if (o.b == 0) { qid[s] = nq++; nreads[s] = 2; }
-      } else if (o.c == 0) {
-        tid[s] = ntr++; nreads[s] = 4;
-      }
-    }
-  }
-  constexpr int pending(int s, int R) const {
-    int c = 0;
-    for (int x = s + 1; x <= s + R && x < NOPS; ++x) c += nreads[x];
-    return c;
-  }
-};
-template <int N, int NSQ, int NDB>
-struct Hold { static constexpr Sched<N, NSQ, NDB> v{}; };
-}  // namespace fw2
-
-// off by default: at cfg2 (N = 2, dv = 128) the O^T accumulators of two blocks take all 256
-// AGPRs and the stream spills (1.4 KB of scratch per lane); kept for smaller N * dv
-#ifndef DTA_FWD2
-#define DTA_FWD2 0
-#endif
-template <class E, int HS, int N, int DV>
-struct Fw2Cfg {
-  static constexpr int NW = 4, BM = 256, BN = 64;
-  static constexpr int nQ = N * BM * HS, nK = N * BN * HS, nV = BN * DV;
-  static constexpr int NS = ring_stages(nQ * (int)sizeof(E), (nK + nV) * (int)sizeof(E));
-  static constexpr int bytes = (nQ + NS * (nK + nV)) * (int)sizeof(E);
-  static constexpr int aregs = 2 * N * (DV / 32) * 16;      // O_i^T of both blocks
-  static constexpr bool shape_ok = DTA_FWD2 && std::is_same<E, __bf16>::value && (HS == 32 || HS == 64 || HS == 128) &&
-                                   DV == 2 * HS && N >= 2 && aregs <= 256 && bytes <= 160 * 1024 &&
-                                   KvRing<E, HS, N, DV, BN, NW>::ok;
-  template <bool S, int = 0> struct Sok { static constexpr bool v = false; };
-  template <int X> struct Sok<true, X> { static constexpr bool v = fw2::Hold<N, HS / 16, DV / 32>::v.ok; };
-  static constexpr bool ok = Sok<shape_ok>::v;
-};
-
-template <class E, int HS, int N, int DV>
-__global__ __launch_bounds__(256, 1)
-void attn_fwd2_kernel(FwdParams p) {
-  using O = Ops<E>;
-  using frag = typename O::frag;
-  using CF = Fw2Cfg<E, HS, N, DV>;
-  constexpr int NW = CF::NW, BM = CF::BM, BN = CF::BN, NTHR = NW * 64, KS = O::KSTEP;
-  constexpr int NSQ = HS / KS, NDB = DV / 32, NKB = 2, NS = CF::NS;
-  constexpr int ROWB = HS * (int)sizeof(E), VROWB = DV * (int)sizeof(E);
-  constexpr int R = DTA_DQ2_R;
-  using SCH = fw2::Hold<N, NSQ, NDB>;
-  using SD = fw2::Sched<N, NSQ, NDB>;
-  constexpr int NOPS = SD::NOPS, U = 2 * N;
-  static_assert(SCH::v.ok, "forward2 schedule");
-  constexpr float LSMAX = std::is_same<E, _Float16>::value ? 0x1p15f : 0x1p60f;
-
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  E* Qs = reinterpret_cast<E*>(smem);   // [N][BM][HS]
-  E* Kb = Qs + CF::nQ;                  // [NS][N][BN][HS]
-  E* Vb = Kb + NS * CF::nK;             // [NS][BN][DV]
-
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  int tid = threadIdx.x, lane = tid & 63;
-  int hf = lane >> 5, c32 = lane & 31;
-  int bx, by, bz, lin;
-  lpt_order(bx, by, bz, lin);
-  const int qt = gridDim.x - 1 - bx;
-  const int hh = by, b = bz;
-  const int T = p.T;
-  const int q0 = qt * BM, qw0 = q0 + wave * 64;
-  const E* gq = reinterpret_cast<const E*>(p.q.p) + b * p.q.sb + hh * p.q.sh;
-  const E* gk = reinterpret_cast<const E*>(p.k.p) + b * p.k.sb + hh * p.k.sh;
-  const E* gv = reinterpret_cast<const E*>(p.v.p) + b * p.v.sb + hh * p.v.sh;
-  const int kend = min(T, q0 + BM);
-  const int ntiles = (kend + BN - 1) / BN;
-  using KR = KvRing<E, HS, N, DV, BN, NW>;
-  uint32_t doff[KR::MYP];
-  KR::offsets(p.k.st, p.k.si, p.v.st, wave, lane, doff);
-  auto stage_kv = [&](int kt, int buf) {
-    KR::issue_pre(gk, p.k.st, gv, p.v.st, kt * BN, T, Kb + buf * CF::nK, Vb + buf * CF::nV, wave, doff);
-  };
-  const int tile_pieces = KR::pieces(wave);
-#pragma unroll
-  for (int i = 0; i < N; ++i) stage<E, HS, BM, HS, NTHR>(Qs + i * BM * HS, gq + i * p.q.si, p.q.st, q0, T - 1, tid);
-
-  f32x16 acc[U][NDB];
-  MfmaHold hold{};
-  float m[U], l[U];
-  float bad = 0.f;
-  const bool wave_live = qw0 < T;
-  const int nfull = wave_live ? min(ntiles, min(qw0 / BN, T / BN)) : 0;
-  const int nlive = wave_live ? min(ntiles, qw0 / BN + 1) : 0;
-  int LrK = row_lane<ROWB>(lane), LtV = tr_lane<VROWB>(lane);
-
-  // S^T chain of one unit (straight code: first tile and the max pre-pass)
-  auto s_chain = [&](auto U_, unsigned bK, unsigned bQ, f32x16 (&s)[NKB]) {
-    constexpr int u = decltype(U_)::value, i = SD::ui(u), qb = SD::uq(u);
-#pragma unroll
-    for (int kb = 0; kb < NKB; ++kb) s[kb] = f32x16{};
-    sfor<NSQ>([&](auto ST) {
-      constexpr int st = decltype(ST)::value;
-      i32x4 qv, k0v, k1v;
-      ds128<i * BM * ROWB + qb * 32 * ROWB>(qv, bQ ^ (32 * st));
-      ds128<i * BN * ROWB>(k0v, bK ^ (32 * st));
-      ds128<i * BN * ROWB + 32 * ROWB>(k1v, bK ^ (32 * st));
-      lgkm_wait<0>();
-      asm volatile("" : "+v"(qv), "+v"(k0v), "+v"(k1v));
-      s[0] = O::mma(__builtin_bit_cast(frag, k0v), __builtin_bit_cast(frag, qv), s[0]);
-      s[1] = O::mma(__builtin_bit_cast(frag, k1v), __builtin_bit_cast(frag, qv), s[1]);
-    });
-  };
-  auto lims = [&](int k0, int (&lim)[2]) {
-#pragma unroll
-    for (int qb = 0; qb < 2; ++qb) lim[qb] = min(qw0 + 32 * qb + (lane & 31), T - 1) - k0 - 4 * (lane >> 5);
-  };
-  auto pv_unit = [&](auto U_, unsigned tV, const frag (&pk)[NKB * 2]) {
-    constexpr int u = decltype(U_)::value;
-    sfor<NDB>([&](auto D) {
-      constexpr int d = decltype(D)::value;
-      lds64 r[NKB][4];
-      sfor<NKB>([&](auto KB) { tr_issue<VROWB, 32 * decltype(KB)::value>(r[decltype(KB)::value], tV ^ (64 * d), tV ^ (64 * d + 32)); });
-      lgkm_pin<NKB>(r);
-#pragma unroll
-      for (int kb = 0; kb < NKB; ++kb) {
-        mfma_agpr<true>(acc[u][d], tr_frag<E>(r[kb], 0), pk[kb * 2 + 0], hold);
-        mfma_agpr<false>(acc[u][d], tr_frag<E>(r[kb], 1), pk[kb * 2 + 1], hold);
-      }
-    });
-  };
-  // first tile of a pass: S^T, (pass 0) the per-row maximum, P, the row sums, O^T += V^T P^T
-  auto first_tile = [&](int kt, bool setmax, auto MASKED) {
-    constexpr bool MASK = decltype(MASKED)::value;
-    const int buf = kt % NS, k0 = kt * BN;
-    const unsigned kbase = lds_addr(Kb + buf * CF::nK), vbase = lds_addr(Vb + buf * CF::nV);
-    const unsigned bK = LrK + kbase, tV = LtV + vbase, bQ = LrK + lds_addr(Qs) + wave * 64 * ROWB;
-    int lim[2];
-    lims(k0, lim);
-    sfor<U>([&](auto U_) {
-      constexpr int u = decltype(U_)::value, qb = SD::uq(u);
-      f32x16 s[NKB];
-      s_chain(U_, bK, bQ, s);
-      if constexpr (MASK) {
-#pragma unroll
-        for (int kb = 0; kb < NKB; ++kb)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) s[kb][r] = (kb * 32 + (r & 3) + 8 * (r >> 2) > lim[qb]) ? -INFINITY : s[kb][r];
-      }
-      if (setmax) {
-        float mx = -INFINITY;
-#pragma unroll
-        for (int kb = 0; kb < NKB; ++kb)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kb][r]);
-        m[u] = wave_max_halves(mx) * p.sl2;
-      }
-      frag pk[NKB * 2];
-      float ls = 0.f;
-#pragma unroll
-      for (int kb = 0; kb < NKB; ++kb) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          s[kb][r] = exp2_fast(fmaf(s[kb][r], p.sl2, -m[u]));
-          ls += s[kb][r];
-        }
-        pk[kb * 2 + 0] = O::template pack<0>(s[kb]);
-        pk[kb * 2 + 1] = O::template pack<1>(s[kb]);
-      }
-      l[u] += ls;
-      bad = (ls <= LSMAX) ? bad : 1.f;
-      pv_unit(U_, tV, pk);
-    });
-  };
-  // later tiles: the scheduled stream
-  auto body = [&](int kt, auto MASKED) {
-    constexpr bool MASK = decltype(MASKED)::value;
-    asm volatile("" : "+v"(LrK), "+v"(LtV));
-    const int buf = kt % NS, k0 = kt * BN;
-    const unsigned kbase = lds_addr(Kb + buf * CF::nK), vbase = lds_addr(Vb + buf * CF::nV);
-    const unsigned bK = LrK + kbase, tV = LtV + vbase, bQ = LrK + lds_addr(Qs) + wave * 64 * ROWB;
-    int lim[2];
-    lims(k0, lim);
-    f32x16 sa[SD::SR][NKB];
-    frag pk[SD::PR][NKB * 2];
-    float lt[U];
-    constexpr int RBN = R + 1, RQN = (R + 1) / 2 + 1, RTN = (R + 1) / 2 + 1;
-    i32x4 rb[RBN], rq[RQN];
-    lds64 rt[RTN][4];
-    auto issue = [&](auto S_) {
-      constexpr int s = decltype(S_)::value;
-      constexpr fw2::Op o = SCH::v.ops[s];
-      if constexpr (o.kind == fw2::SC) {
-        ds128<o.i * BN * ROWB + o.b * 32 * ROWB>(rb[SCH::v.rid[s] % RBN], bK ^ (32 * o.a));
-        if constexpr (o.b == 0) ds128<o.i * BM * ROWB + o.qb * 32 * ROWB>(rq[SCH::v.qid[s] % RQN], bQ ^ (32 * o.a));
-      } else if constexpr (o.c == 0) {
-        tr_issue<VROWB, 32 * o.b>(rt[SCH::v.tid[s] % RTN], tV ^ (64 * o.a), tV ^ (64 * o.a + 32));
-      }
-    };
-    auto piece = [&](auto PU) {
-      constexpr int u = decltype(PU)::value / fw2::PIECES, j = decltype(PU)::value % fw2::PIECES;
-      constexpr int qb = SD::uq(u), kb = j / 8, r0 = (j % 8) * 2, su = u % SD::SR;
-      if constexpr (j == 0) lt[u] = 0.f;
-#pragma unroll
-      for (int r = r0; r < r0 + 2; ++r) {
-        float x = sa[su][kb][r];
-        if constexpr (MASK) x = (kb * 32 + (r & 3) + 8 * (r >> 2) > lim[qb]) ? -INFINITY : x;
-        const float e = exp2_fast(fmaf(x, p.sl2, -m[u]));
-        sa[su][kb][r] = e;
-        lt[u] += e;
-      }
-      if constexpr (j % 4 == 3) pk[u % SD::PR][kb * 2 + (j % 8) / 4] = O::template pack<(j % 8) / 4>(sa[su][kb]);
-      if constexpr (j == fw2::PIECES - 1) {
-        l[u] += lt[u];
-        bad = (lt[u] <= LSMAX) ? bad : 1.f;
-      }
-    };
-    sfor<(R < NOPS ? R : NOPS)>([&](auto S_) { issue(S_); });
-    sfor<NOPS>([&](auto S_) {
-      constexpr int s = decltype(S_)::value;
-      constexpr fw2::Op o = SCH::v.ops[s];
-      if constexpr (s + R < NOPS) issue(std::integral_constant<int, s + R>{});
-      if constexpr (SCH::v.nreads[s] > 0) lgkm_wait<SCH::v.pending(s, R)>();
-      if constexpr (o.kind == fw2::SC) {
-        i32x4& kr = rb[SCH::v.rid[s] % RBN];
-        i32x4& qr = rq[(o.b == 0 ? SCH::v.qid[s] : SCH::v.qid[s - 1]) % RQN];
-        asm volatile("" : "+v"(kr), "+v"(qr));
-        f32x16& acc_s = sa[o.u % SD::SR][o.b];
-        acc_s = O::mma(__builtin_bit_cast(frag, kr), __builtin_bit_cast(frag, qr), o.a == 0 ? f32x16{} : acc_s);
-      } else {
-        lds64 (&tr)[4] = rt[(o.c == 0 ? SCH::v.tid[s] : SCH::v.tid[s - 1]) % RTN];
-        if constexpr (o.c == 0) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(tr[j]));
-        }
-        mfma_agpr<(s == SCH::v.p0[o.u])>(acc[o.u][o.a], tr_frag<E>(tr, o.c), pk[o.u % SD::PR][o.b * 2 + o.c], hold);
-      }
-      sfor<SCH::v.npiece[s]>([&](auto K) { piece(std::integral_constant<int, SCH::v.pu[s][decltype(K)::value]>{}); });
-      __builtin_amdgcn_sched_barrier(0);
-    });
-  };
-  auto tail = [&](int kt) {
-    wait_vm(tile_pieces * max(0, min(NS - 2, ntiles - 2 - kt)));
-    lds_barrier();
-  };
-  auto prologue = [&]() {
-    for (int j = 0; j < NS - 1; ++j)
-      if (j < ntiles) stage_kv(j, j);
-    wait_vm(tile_pieces * max(0, min(NS - 1, ntiles) - 1));
-    lds_barrier();
-  };
-  // pass 0: the first tile's maximum; pass 1 (a flagged workgroup): the exact maxima first
-  for (int pass = 0; pass < 2; ++pass) {
-    if (pass == 1) {
-      // rows' exact maxima: S^T over every live tile
-#pragma unroll
-      for (int u = 0; u < U; ++u) m[u] = -INFINITY;
-      prologue();
-      for (int kt = 0; kt < ntiles; ++kt) {
-        if (kt + NS - 1 < ntiles) stage_kv(kt + NS - 1, (kt + NS - 1) % NS);
-        if (kt < nlive) {
-          const int buf = kt % NS, k0 = kt * BN;
-          const unsigned bK = LrK + lds_addr(Kb + buf * CF::nK), bQ = LrK + lds_addr(Qs) + wave * 64 * ROWB;
-          int lim[2];
-          lims(k0, lim);
-          sfor<U>([&](auto U_) {
-            constexpr int u = decltype(U_)::value, qb = SD::uq(u);
-            f32x16 s[NKB];
-            s_chain(U_, bK, bQ, s);
-            float mx = -INFINITY;
-#pragma unroll
-            for (int kb = 0; kb < NKB; ++kb)
-#pragma unroll
-              for (int r = 0; r < 16; ++r) mx = fmaxf(mx, (kb * 32 + (r & 3) + 8 * (r >> 2) > lim[qb]) ? -INFINITY : s[kb][r]);
-            m[u] = fmaxf(m[u], wave_max_halves(mx) * p.sl2);
-          });
-        }
-        tail(kt);
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      l[u] = 0.f;
-#pragma unroll
-      for (int d = 0; d < NDB; ++d) acc[u][d] = f32x16{};
-    }
-    bad = 0.f;
-    prologue();
-    for (int kt = 0; kt < ntiles; ++kt) {
-      if (kt + NS - 1 < ntiles) stage_kv(kt + NS - 1, (kt + NS - 1) % NS);
-      if (kt == 0 && pass == 0) {
-        if (nfull > 0) first_tile(0, true, std::false_type{});
-        else if (nlive > 0) first_tile(0, true, std::true_type{});
-      } else if (kt < nfull) {
-        body(kt, std::false_type{});
-      } else if (kt < nlive) {
-        body(kt, std::true_type{});
-      }
-      tail(kt);
-    }
-    if (pass == 1) break;
-    int* flag = reinterpret_cast<int*>(Kb);
-    const bool mine = __any(wave_live && bad != 0.f);
-    if (lane == 0) flag[wave] = mine ? 1 : 0;
-    lds_barrier();
-    bool any = false;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) any |= flag[w] != 0;
-    lds_barrier();
-    if (!any) break;
-  }
-  dq2_acc_fence();
-  acc_pin(acc);
-  mfma_release(hold);
-
-  if (!wave_live) return;
-#pragma unroll
-  for (int qb = 0; qb < 2; ++qb) {
-    const int qrow = qw0 + 32 * qb + c32;
-    if (qrow >= T) continue;
-    float inv[N];
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-      const int u = 2 * i + qb;
-      const float lt = wave_sum_halves(l[u]);
-      inv[i] = 1.f / lt;
-      if (hf == 0) p.lse[(((int64_t)i * p.B + b) * p.H + hh) * T + qrow] = -(m[u] + __builtin_log2f(lt));
-    }
-    E* go = reinterpret_cast<E*>(p.o.p) + b * p.o.sb + (int64_t)qrow * p.o.st + hh * p.o.sh;
-    const int64_t gob = b * p.obr.sb + (int64_t)qrow * p.obr.st + hh * p.obr.sh;
-#pragma unroll
-    for (int d = 0; d < NDB; ++d)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int e = d * 32 + 8 * g + 4 * hf;
-        float o0 = 0.f, o1 = 0.f, o2 = 0.f, o3 = 0.f;
-#pragma unroll
-        for (int i = 0; i < N; ++i) {
-          const int u = 2 * i + qb;
-          const float a0 = acc[u][d][4 * g + 0] * inv[i], a1 = acc[u][d][4 * g + 1] * inv[i];
-          const float a2 = acc[u][d][4 * g + 2] * inv[i], a3 = acc[u][d][4 * g + 3] * inv[i];
-          store_ob4(p.obr.p, gob + i * p.obr.si + e, p.ob16, a0, a1, a2, a3);
-          const float c = p.coef[hh * p.cst + i];
-          o0 = fmaf(c, a0, o0); o1 = fmaf(c, a1, o1); o2 = fmaf(c, a2, o2); o3 = fmaf(c, a3, o3);
-        }
-        store4<E>(go + e, o0, o1, o2, o3);
-      }
-  }
-}
-
 // ------------------------------- forward: key tiles software-pipelined ---
 // attn_fwd3_kernel: the fixed-reference-maximum forward (FAST, as attn_fwd) for one wave per
 // SIMD with the key-tile loop software-pipelined, so the matrix pipe always has work that
@@ -3829,9 +3402,7 @@ struct Plan {
                              DkdvCfg<E, HS, N, DV, KVW, KPR, DkdvWaves<E, HS, N, DV>::gr>::bytes <= 160 * 1024;
 };
 
-int launch_attn_fwd2_bf16(const FwdParams& p, hipStream_t st); // attn_bf16_dq2.hip
 int launch_attn_fwd3_bf16(const FwdParams& p, hipStream_t st); // attn_bf16_dq2.hip
-static inline bool fwd2_env();
 static inline bool fwd3_env();
 template <class E, int HS, int N, int DV_, bool DROP>
 int launch_fwd_t(const FwdParams& p, hipStream_t st) {
@@ -3870,10 +3441,6 @@ int launch_fwd_t(const FwdParams& p, hipStream_t st) {
       return launch_attn_fwd3_bf16(q, st);
     }
   }
-  if constexpr (Fw2Cfg<E, HS, N, PL::DV>::ok && !DROP) {
-    // one wave per SIMD, two 32-row blocks per wave (attn_fwd2_kernel, unit attn_bf16_dq2.hip)
-    if (!p.rope && kv_layout_ok(p, (int)sizeof(E)) && fwd2_env()) return launch_attn_fwd2_bf16(p, st);
-  }
   const int nsp = (N == 1 && p.bsplit > 1) ? p.bsplit : 1;
   dim3 grid((p.T + NW * 32 - 1) / (NW * 32), p.H * nsp * (PL::DV / DVC), p.B);
   auto run = [&](auto SRDV) -> int {
@@ -3903,14 +3470,6 @@ int launch_dkdv2_t(const BwdParams& p, hipStream_t st) {
   return (int)hipGetLastError();
 }
 template <class E, int HS, int N, int DV>
-int launch_fwd2_t(const FwdParams& p, hipStream_t st) {
-  using C2 = Fw2Cfg<E, HS, N, DV>;
-  auto kern = attn_fwd2_kernel<E, HS, N, DV>;
-  if (int e = set_smem(kern, C2::bytes)) return e;
-  hipLaunchKernelGGL(kern, dim3((p.T + C2::BM - 1) / C2::BM, p.H, p.B), dim3(256), C2::bytes, st, p);
-  return (int)hipGetLastError();
-}
-template <class E, int HS, int N, int DV>
 int launch_fwd3_t(const FwdParams& p, hipStream_t st) {
   using C3 = Fw3Cfg<E, HS, N, DV>;
   auto kern = attn_fwd3_kernel<E, HS, N, DV>;
@@ -3923,14 +3482,6 @@ int launch_fwd3_t(const FwdParams& p, hipStream_t st) {
 static inline bool fwd3_env() {
   static const bool v = [] {
     const char* s = getenv("DTA_FWD3");
-    return s && *s == '1';           // opt-in until verified on the GPU
-  }();
-  return v;
-}
-// DTA_FWD2 = 0 in the environment keeps attn_fwd_kernel where attn_fwd2_kernel is built
-static inline bool fwd2_env() {
-  static const bool v = [] {
-    const char* s = getenv("DTA_FWD2");
     return s && *s == '1';           // opt-in until verified on the GPU
   }();
   return v;

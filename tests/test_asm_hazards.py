@@ -1,4 +1,4 @@
-"""The inline-asm MFMA kernels (attn_fwd2 / attn_fwd3 / attn_dq2 / attn_dkdv2) read no
+"""The inline-asm MFMA kernels (attn_fwd3 / attn_dq2 / attn_dkdv2) read no
 accumulator before its MFMA has landed and spill nothing (tools/asm_hazards.py: the
 compiler does not see an asm MFMA's latency, so a copy or spill it places right after one
 reads the old value -- the failure the first attn_fwd3 build had).  CPU only: hipcc -S."""

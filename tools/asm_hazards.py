@@ -1,5 +1,5 @@
 """Static check of the kernels whose accumulators are written by inline-asm MFMAs
-(mfma_agpr: attn_fwd2 / attn_fwd3 / attn_dq2 / attn_dkdv2).
+(mfma_agpr: attn_fwd3 / attn_dq2 / attn_dkdv2).
 
 The compiler does not see an asm MFMA's latency: it treats the accumulator as written
 when the asm statement issues.  Any instruction it places soon after that reads those
@@ -16,7 +16,7 @@ import re
 import subprocess
 import sys
 
-KERNELS = re.compile(r"^(_ZN3dta\d+attn_(?:fwd2|fwd3|dq2|dkdv2)_kernel\w*):", re.M)
+KERNELS = re.compile(r"^(_ZN3dta\d+attn_(?:fwd3|dq2|dkdv2)_kernel\w*):", re.M)
 STORES = ("scratch_store", "global_store", "buffer_store", "ds_write")
 WAIT_STATES = 18
 
