@@ -24,15 +24,19 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / 64;
 
-template <class E>
+#ifndef DTA_DEC_NT
+#define DTA_DEC_NT 0       // 1: the K/V cache stream read with non-temporal loads
+#endif
+template <class E, bool NT = false>
 __device__ __forceinline__ void ld8f(const E* p, float* f) {
   if constexpr (sizeof(E) == 2) {
     typedef E v8 __attribute__((ext_vector_type(8)));
-    const v8 v = *reinterpret_cast<const v8*>(p);
+    const v8 v = NT ? __builtin_nontemporal_load(reinterpret_cast<const v8*>(p)) : *reinterpret_cast<const v8*>(p);
 #pragma unroll
     for (int j = 0; j < 8; ++j) f[j] = (float)v[j];
   } else {
-    const f32x4 a = *reinterpret_cast<const f32x4*>(p), b = *reinterpret_cast<const f32x4*>(p + 4);
+    const f32x4* q = reinterpret_cast<const f32x4*>(p);
+    const f32x4 a = NT ? __builtin_nontemporal_load(q) : q[0], b = NT ? __builtin_nontemporal_load(q + 1) : q[1];
 #pragma unroll
     for (int j = 0; j < 4; ++j) { f[j] = a[j]; f[j + 4] = b[j]; }
   }
@@ -198,7 +202,7 @@ __global__ __launch_bounds__(kThreads) void decode_split_kernel(DecodeParams p) 
 #pragma unroll
       for (int i = 0; i < N; ++i) {
         float f[8];
-        ld8f<E>(kp + i * p.k.si, f);
+        ld8f<E, DTA_DEC_NT>(kp + i * p.k.si, f);
         float d = 0.f;
 #pragma unroll
         for (int u = 0; u < 8; ++u) d = fmaf(q[i][u], f[u], d);
@@ -242,7 +246,7 @@ __global__ __launch_bounds__(kThreads) void decode_split_kernel(DecodeParams p) 
     for (int u = 0; u < 8; ++u) acc[i][u] = 0.f;
   for (int jj = g; jj < nk; jj += G) {
     float f[8];
-    ld8f<E>(gv + (int64_t)(j0 + jj) * p.v.st, f);
+    ld8f<E, DTA_DEC_NT>(gv + (int64_t)(j0 + jj) * p.v.st, f);
 #pragma unroll
     for (int i = 0; i < N; ++i) {
       const float e = sc[i][jj];
