@@ -500,7 +500,10 @@ static inline int grid_for(int64_t items) {
 #endif
 // blocks of the LN backward: enough waves in flight to cover HBM latency, few enough
 // that the per-block column partials stay small (dta_ln_bwd_workspace_bytes)
-int ln_bwd_blocks(int64_t rows) { return (int)std::min<int64_t>((rows + 7) / 8, 1024); }
+#ifndef DTA_LN_BWD_MAXBLK
+#define DTA_LN_BWD_MAXBLK 1024   // workgroups of the backward: occupancy vs partial rows to reduce
+#endif
+int ln_bwd_blocks(int64_t rows) { return (int)std::min<int64_t>((rows + 7) / 8, DTA_LN_BWD_MAXBLK); }
 int64_t ln_bwd_workspace_floats(int64_t rows, int64_t C) { return ((int64_t)ln_bwd_blocks(rows) + kLnChunks) * 2 * C; }
 
 template <class E>
