@@ -275,7 +275,10 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnParams p) {
 // buffered LDS slot, one barrier per row.  The next row's x / dy are loaded before
 // the current row's math.  ~60 VGPRs: 4 workgroups (16 waves) per CU, where the
 // wave-per-row kernel above holds 222 registers for C = 2048 (8 waves per CU).
-template <class E, int CHB, class Y = E>
+#ifndef DTA_LN_BWD_RPI
+#define DTA_LN_BWD_RPI 1         // rows per barrier (each workgroup step)
+#endif
+template <class E, int CHB, class Y = E, int RPI = DTA_LN_BWD_RPI>
 __global__ __launch_bounds__(256) void ln_bwd_rb_kernel(LnParams p) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   float dwp[CHB][8], dbp[CHB][8];
@@ -284,34 +287,43 @@ __global__ __launch_bounds__(256) void ln_bwd_rb_kernel(LnParams p) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) { dwp[c][j] = 0.f; dbp[c][j] = 0.f; }
   const float inv_c = 1.f / (float)p.C;
-  __shared__ float red[2][4][2];
+  __shared__ float red[2][RPI][4][2];
   // raw (unconverted) vectors of 8 elements: one s16x8 for 16-bit, two f32x4 for fp32
   constexpr bool P16 = sizeof(E) == 2, Y16 = sizeof(Y) == 2;
   typedef typename std::conditional<P16, s16x8, f32x4>::type RT;
   typedef typename std::conditional<Y16, s16x8, f32x4>::type RY;
   constexpr int NR = P16 ? 1 : 2, NY = Y16 ? 1 : 2;
-  RT xr[2][CHB][NR];
-  RY dr[2][CHB][NY];
-  float mr[2], rr[2];
-  auto load = [&](auto S, int64_t r) {
+  RT xr[2][RPI][CHB][NR];
+  RY dr[2][RPI][CHB][NY];
+  float mr[2][RPI], rr[2][RPI];
+  const int64_t stride = gridDim.x;
+  // rows r0 + q*stride, q < RPI; past the last row the last row is re-read (masked in the
+  // math): a load behind a branch would leave the wait counters unknown at the join
+  auto load = [&](auto S, int64_t r0) {
     constexpr int s = decltype(S)::value;
-    // the row statistics first: a load issued after the next row's prefetch would make
-    // its wait (vmcnt counts in order) drain that prefetch too
-    mr[s] = p.mean[r];
-    rr[s] = p.rstd[r];
-    const E* x = reinterpret_cast<const E*>(p.x) + r * p.xs;
-    const Y* dy = reinterpret_cast<const Y*>(p.dy) + r * p.dys;
-    // unconditional loads (lanes past C read column 0, masked in the math): a load behind a
-    // divergent branch leaves the wait counters unknown at the join, and the compiler
-    // then waits for every load in flight -- the next row's prefetch included
 #pragma unroll
-    for (int c = 0; c < CHB; ++c) {
-      const int col0 = (c * 256 + t) * 8;
-      const int col = col0 < p.C ? col0 : 0;
+    for (int q = 0; q < RPI; ++q) {
+      const int64_t r = min(r0 + q * stride, p.rows - 1);
+      // the row statistics first: a load issued after the next row's prefetch would make
+      // its wait (vmcnt counts in order) drain that prefetch too
+      mr[s][q] = p.mean[r];
+      rr[s][q] = p.rstd[r];
+    }
 #pragma unroll
-      for (int k = 0; k < NR; ++k) xr[s][c][k] = *reinterpret_cast<const RT*>(x + col + k * 4);
+    for (int q = 0; q < RPI; ++q) {
+      const int64_t r = min(r0 + q * stride, p.rows - 1);
+      const E* x = reinterpret_cast<const E*>(p.x) + r * p.xs;
+      const Y* dy = reinterpret_cast<const Y*>(p.dy) + r * p.dys;
+      // unconditional loads (lanes past C read column 0, masked in the math)
 #pragma unroll
-      for (int k = 0; k < NY; ++k) dr[s][c][k] = *reinterpret_cast<const RY*>(dy + col + k * 4);
+      for (int c = 0; c < CHB; ++c) {
+        const int col0 = (c * 256 + t) * 8;
+        const int col = col0 < p.C ? col0 : 0;
+#pragma unroll
+        for (int k = 0; k < NR; ++k) xr[s][q][c][k] = ldv(reinterpret_cast<const RT*>(x + col + k * 4));
+#pragma unroll
+        for (int k = 0; k < NY; ++k) dr[s][q][c][k] = ldv(reinterpret_cast<const RY*>(dy + col + k * 4));
+      }
     }
   };
   auto cvt = [&](auto T16, const auto& v, float* f) {
@@ -323,7 +335,6 @@ __global__ __launch_bounds__(256) void ln_bwd_rb_kernel(LnParams p) {
       for (int j = 0; j < 4; ++j) { f[j] = v[0][j]; f[j + 4] = v[1][j]; }
     }
   };
-  const int64_t stride = gridDim.x;
   int par = 0;
   // this thread's LN weights, the same for every row: loaded once (a per-row load issued
   // behind the next row's prefetch would drain it at its wait)
@@ -334,67 +345,77 @@ __global__ __launch_bounds__(256) void ln_bwd_rb_kernel(LnParams p) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) wv[c][j] = col < p.C ? p.w[col + j] : 0.f;
   }
-  auto body = [&](auto S, int64_t r) {
+  auto body = [&](auto S, int64_t r0) {
     constexpr int s = decltype(S)::value;
-    const float mean = mr[s], rstd = rr[s];
-    if (r + stride < p.rows) load(std::integral_constant<int, 1 - s>{}, r + stride);   // next row in flight
-    float xh[CHB][8], g[CHB][8];
-    float sg = 0.f, sgx = 0.f;
+    if (r0 + RPI * stride < p.rows) load(std::integral_constant<int, 1 - s>{}, r0 + RPI * stride);   // next rows in flight
+    float xh[RPI][CHB][8], g[RPI][CHB][8];
 #pragma unroll
-    for (int c = 0; c < CHB; ++c) {
-      const bool ok = (c * 256 + t) * 8 < p.C;
-      float xv[8], dv[8];
-      cvt(E{}, xr[s][c], xv);
-      cvt(Y{}, dr[s][c], dv);
+    for (int q = 0; q < RPI; ++q) {
+      const bool live = r0 + q * stride < p.rows;      // workgroup-uniform
+      const float mean = mr[s][q], rstd = rr[s][q];
+      float sg = 0.f, sgx = 0.f;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        xh[c][j] = ok ? (xv[j] - mean) * rstd : 0.f;
-        const float dys = ok ? dv[j] * p.out_scale : 0.f;
-        dwp[c][j] = fmaf(dys, xh[c][j], dwp[c][j]);
-        dbp[c][j] += dys;
-        g[c][j] = dys * wv[c][j];
-        sg += g[c][j];
-        sgx = fmaf(g[c][j], xh[c][j], sgx);
+      for (int c = 0; c < CHB; ++c) {
+        const bool ok = live && (c * 256 + t) * 8 < p.C;
+        float xv[8], dv[8];
+        cvt(E{}, xr[s][q][c], xv);
+        cvt(Y{}, dr[s][q][c], dv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          xh[q][c][j] = ok ? (xv[j] - mean) * rstd : 0.f;
+          const float dys = ok ? dv[j] * p.out_scale : 0.f;
+          dwp[c][j] = fmaf(dys, xh[q][c][j], dwp[c][j]);
+          dbp[c][j] += dys;
+          g[q][c][j] = dys * wv[c][j];
+          sg += g[q][c][j];
+          sgx = fmaf(g[q][c][j], xh[q][c][j], sgx);
+        }
       }
+      sg = wave_sum(sg);
+      sgx = wave_sum(sgx);
+      if (lane == 0) { red[par][q][wave][0] = sg; red[par][q][wave][1] = sgx; }
     }
-    sg = wave_sum(sg);
-    sgx = wave_sum(sgx);
-    if (lane == 0) { red[par][wave][0] = sg; red[par][wave][1] = sgx; }
-    // LDS-only barrier: __syncthreads() would also wait for the next row's prefetch
+    // LDS-only barrier: __syncthreads() would also wait for the next rows' prefetch
     __builtin_amdgcn_s_waitcnt(0xC07F);          // lgkmcnt(0)
     __builtin_amdgcn_s_barrier();
-    const float mg = (red[par][0][0] + red[par][1][0] + red[par][2][0] + red[par][3][0]) * inv_c;
-    const float mgx = (red[par][0][1] + red[par][1][1] + red[par][2][1] + red[par][3][1]) * inv_c;
-    par ^= 1;
-    E* dx = reinterpret_cast<E*>(p.dx) + r * p.dxs;
 #pragma unroll
-    for (int c = 0; c < CHB; ++c) {
-      const int col = (c * 256 + t) * 8;
-      if (col < p.C) {
-        float o[8];
+    for (int q = 0; q < RPI; ++q) {
+      const int64_t r = r0 + q * stride;
+      if (r >= p.rows) break;
+      const float rstd = rr[s][q];
+      const float mg = (red[par][q][0][0] + red[par][q][1][0] + red[par][q][2][0] + red[par][q][3][0]) * inv_c;
+      const float mgx = (red[par][q][0][1] + red[par][q][1][1] + red[par][q][2][1] + red[par][q][3][1]) * inv_c;
+      E* dx = reinterpret_cast<E*>(p.dx) + r * p.dxs;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = rstd * (g[c][j] - mg - xh[c][j] * mgx);
-        if constexpr (std::is_same<E, float>::value && Y16) {
-          if (p.dres) {                        // residual fusion: + the residual branch's gradient
-            float d[8];
-            ld8<float>(p.dres + r * p.dress + col, d);
+      for (int c = 0; c < CHB; ++c) {
+        const int col = (c * 256 + t) * 8;
+        if (col < p.C) {
+          float o[8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) o[j] += d[j];
+          for (int j = 0; j < 8; ++j) o[j] = rstd * (g[q][c][j] - mg - xh[q][c][j] * mgx);
+          if constexpr (std::is_same<E, float>::value && Y16) {
+            if (p.dres) {                        // residual fusion: + the residual branch's gradient
+              float d[8];
+              ld8<float>(p.dres + r * p.dress + col, d);
+#pragma unroll
+              for (int j = 0; j < 8; ++j) o[j] += d[j];
+            }
+            if (p.dx16) st8<Y>(reinterpret_cast<Y*>(p.dx16) + r * p.dx16s + col, o);
           }
-          if (p.dx16) st8<Y>(reinterpret_cast<Y*>(p.dx16) + r * p.dx16s + col, o);
+          st8<E>(dx + col, o);
         }
-        st8<E>(dx + col, o);
       }
     }
+    par ^= 1;
   };
   int64_t r = blockIdx.x;
   if (r < p.rows) load(std::integral_constant<int, 0>{}, r);
   while (r < p.rows) {
     body(std::integral_constant<int, 0>{}, r);
-    r += stride;
+    r += RPI * stride;
     if (r >= p.rows) break;
     body(std::integral_constant<int, 1>{}, r);
-    r += stride;
+    r += RPI * stride;
   }
 #pragma unroll
   for (int c = 0; c < CHB; ++c) {
