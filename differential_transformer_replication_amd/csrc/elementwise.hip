@@ -522,7 +522,7 @@ static inline int grid_for(int64_t items) {
 // blocks of the LN backward: enough waves in flight to cover HBM latency, few enough
 // that the per-block column partials stay small (dta_ln_bwd_workspace_bytes)
 #ifndef DTA_LN_BWD_MAXBLK
-#define DTA_LN_BWD_MAXBLK 1024   // workgroups of the backward: occupancy vs partial rows to reduce
+#define DTA_LN_BWD_MAXBLK 512    // workgroups of the backward: occupancy vs partial rows to reduce (1024: +2%, r04_ab_ln_rpi_blocks.json)
 #endif
 int ln_bwd_blocks(int64_t rows) { return (int)std::min<int64_t>((rows + 7) / 8, DTA_LN_BWD_MAXBLK); }
 int64_t ln_bwd_workspace_floats(int64_t rows, int64_t C) { return ((int64_t)ln_bwd_blocks(rows) + kLnChunks) * 2 * C; }
