@@ -83,11 +83,26 @@ bool attn_supported(int dtype, int hs, int n, int dv) {
   if (n < 1) return false;
   return attn_native(dtype, hs, n, dv) || (n >= 2 && dv == 2 * hs && attn_native(dtype, hs, 1, dv));
 }
-// size of the next branch group of the backward: the largest native branch count <= 4
-int branch_group(int dtype, int hs, int left, int dv) {
-  for (int g = left < 4 ? left : 4; g > 1; --g)
+// size of the next branch group of the backward: the largest native branch count <= cap
+int branch_group(int dtype, int hs, int left, int dv, int cap) {
+  for (int g = left < cap ? left : cap; g > 1; --g)
     if (attn_native(dtype, hs, g, dv)) return g;
   return 1;
+}
+// largest backward branch group per stage.  16-bit dK/dV at head size >= 64 and dQ at
+// head size >= 128 run as groups of <= 2 branches (each group recomputes dP = dO V^T, but
+// the 3- / 4-branch plans have no room for the paired 2-wave-per-SIMD layout: one wave
+// per SIMD with spills); measured per kernel in profiles/r04_bwd_groups.json:
+// dK/dV hs 96 N = 4 11.6 -> 3.4 ms, hs 128 N = 4 dQ 4.0 -> 2.0 ms, hs 64 N = 3 dK/dV
+// 0.46 -> 0.44 ms; head size 32 and dQ at hs <= 96 keep the native plans (faster there).
+// DTA_BWD_GROUP_MAX (A/B builds) overrides both.
+int bwd_group_cap(int dtype, int hs, bool dkdv) {
+#ifdef DTA_BWD_GROUP_MAX
+  return DTA_BWD_GROUP_MAX;
+#else
+  if (dtype == DTA_F32) return 4;
+  return (dkdv ? hs >= 64 : hs >= 128) ? 2 : 4;
+#endif
 }
 }  // namespace dta
 
@@ -277,7 +292,7 @@ int dta_attn_bwd(const dta_attn_bwd_args* a, void* stream) {
   int e = 0;
   if (stages & DTA_BWD_DQ) {
     for (int g0 = 0, ng; g0 < p.N; g0 += ng) {
-      ng = branch_group(a->dtype, p.HS, p.N - g0, p.DV);
+      ng = branch_group(a->dtype, p.HS, p.N - g0, p.DV, bwd_group_cap(a->dtype, p.HS, false));
       if ((e = launch_attn_dq(a->dtype, group(g0, ng), st))) return status(e);
     }
     if (p.dcoef_part &&
@@ -286,7 +301,7 @@ int dta_attn_bwd(const dta_attn_bwd_args* a, void* stream) {
   }
   if (stages & DTA_BWD_DKDV) {
     for (int g0 = 0, ng; g0 < p.N; g0 += ng) {
-      ng = branch_group(a->dtype, p.HS, p.N - g0, p.DV);
+      ng = branch_group(a->dtype, p.HS, p.N - g0, p.DV, bwd_group_cap(a->dtype, p.HS, true));
       if ((e = launch_attn_dkdv(a->dtype, group(g0, ng), st))) return status(e);
     }
   }

@@ -61,7 +61,7 @@ CASES = [  # H, N, hs, T, rope
     # head size 96 (the reference's default TrainingConfig: train.py:60-61, diff_transformer.py:111),
     # N = 4 at head sizes 96 / 128 (dQ 32-key tiles, dK/dV row vectors from global memory)
     (2, 2, 96, 129, False), (1, 1, 96, 200, False), (1, 3, 96, 70, True), (1, 4, 96, 100, True),
-    (1, 4, 128, 97, False), (1, 2, 96, 700, True),
+    (1, 4, 128, 97, False), (1, 2, 96, 700, True), (1, 3, 128, 130, False),
 ]
 
 
