@@ -89,19 +89,22 @@ int branch_group(int dtype, int hs, int left, int dv, int cap) {
     if (attn_native(dtype, hs, g, dv)) return g;
   return 1;
 }
-// largest backward branch group per stage.  16-bit dK/dV at head size >= 64 and dQ at
-// head size >= 128 run as groups of <= 2 branches (each group recomputes dP = dO V^T, but
-// the 3- / 4-branch plans have no room for the paired 2-wave-per-SIMD layout: one wave
-// per SIMD with spills); measured per kernel in profiles/r04_bwd_groups.json:
-// dK/dV hs 96 N = 4 11.6 -> 3.4 ms, hs 128 N = 4 dQ 4.0 -> 2.0 ms, hs 64 N = 3 dK/dV
-// 0.46 -> 0.44 ms; head size 32 and dQ at hs <= 96 keep the native plans (faster there).
-// DTA_BWD_GROUP_MAX (A/B builds) overrides both.
-int bwd_group_cap(int dtype, int hs, bool dkdv) {
+// largest backward branch group.  16-bit backward at head size >= 96, and at head size
+// 64 for N >= 4, runs as groups of <= 2 branches: each group recomputes dP = dO V^T, but
+// the 3- / 4-branch plans have no room for the paired two-waves-per-SIMD layout (one wave
+// per SIMD, with spills).  Measured per kernel in profiles/r04_bwd_groups.json (dQ + dK/dV,
+// bf16): hs 96 N = 4 13.9 -> 5.7 ms, hs 128 N = 4 12.4 -> 4.9 ms, hs 64 N = 4 1.07 ->
+// 1.00 ms, hs 96 N = 3 7.6 -> 4.8 ms; hs 64 N = 3 (0.86 vs 0.88 ms) and head size 32 keep
+// the native plans.  One cap for both stages: attn_dq leaves each group's delta rows
+// relative to the group's first branch (-delta_0 | delta_0 - delta_i), which attn_dkdv
+// reads back group by group.
+// DTA_BWD_GROUP_MAX (A/B builds) overrides it.
+int bwd_group_cap(int dtype, int hs, int n) {
 #ifdef DTA_BWD_GROUP_MAX
   return DTA_BWD_GROUP_MAX;
 #else
   if (dtype == DTA_F32) return 4;
-  return (dkdv ? hs >= 64 : hs >= 128) ? 2 : 4;
+  return (hs >= 96 || (hs >= 64 && n >= 4)) ? 2 : 4;
 #endif
 }
 }  // namespace dta
@@ -290,9 +293,10 @@ int dta_attn_bwd(const dta_attn_bwd_args* a, void* stream) {
     return q;
   };
   int e = 0;
+  const int cap = bwd_group_cap(a->dtype, p.HS, p.N);
   if (stages & DTA_BWD_DQ) {
     for (int g0 = 0, ng; g0 < p.N; g0 += ng) {
-      ng = branch_group(a->dtype, p.HS, p.N - g0, p.DV, bwd_group_cap(a->dtype, p.HS, false));
+      ng = branch_group(a->dtype, p.HS, p.N - g0, p.DV, cap);
       if ((e = launch_attn_dq(a->dtype, group(g0, ng), st))) return status(e);
     }
     if (p.dcoef_part &&
@@ -301,7 +305,7 @@ int dta_attn_bwd(const dta_attn_bwd_args* a, void* stream) {
   }
   if (stages & DTA_BWD_DKDV) {
     for (int g0 = 0, ng; g0 < p.N; g0 += ng) {
-      ng = branch_group(a->dtype, p.HS, p.N - g0, p.DV, bwd_group_cap(a->dtype, p.HS, true));
+      ng = branch_group(a->dtype, p.HS, p.N - g0, p.DV, cap);
       if ((e = launch_attn_dkdv(a->dtype, group(g0, ng), st))) return status(e);
     }
   }
