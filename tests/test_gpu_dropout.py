@@ -78,6 +78,8 @@ DROP_CASES = [  # H, N, hs, T, dv, rope, p
     (1, 2, 64, 700, 128, False, 0.2),
     # branch-split forward (one branch per workgroup + combine) with the mask: N = 3 / 4 at hs = 64
     (2, 3, 64, 150, 128, True, 0.2), (1, 4, 64, 100, 128, False, 0.1),
+    # backward in branch groups of two (head size >= 96, N = 3 / 4)
+    (1, 3, 96, 120, 192, True, 0.2), (1, 4, 128, 90, 256, False, 0.1),
     # branch counts without an N-branch plan (branch-split forward, grouped backward: the
     # mask keys keep the call's branch index and count), a zero-padded head size
     (1, 5, 64, 130, 128, True, 0.2), (1, 6, 32, 100, 64, False, 0.1), (1, 2, 48, 90, 96, False, 0.2),
