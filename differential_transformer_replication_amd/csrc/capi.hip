@@ -89,23 +89,36 @@ int branch_group(int dtype, int hs, int left, int dv, int cap) {
     if (attn_native(dtype, hs, g, dv)) return g;
   return 1;
 }
-// largest backward branch group.  16-bit backward at head size >= 96, and at head size
-// 64 for N >= 4, runs as groups of <= 2 branches: each group recomputes dP = dO V^T, but
-// the 3- / 4-branch plans have no room for the paired two-waves-per-SIMD layout (one wave
-// per SIMD, with spills).  Measured per kernel in profiles/r04_bwd_groups.json (dQ + dK/dV,
-// bf16): hs 96 N = 4 13.9 -> 5.7 ms, hs 128 N = 4 12.4 -> 4.9 ms, hs 64 N = 4 1.07 ->
-// 1.00 ms, hs 96 N = 3 7.6 -> 4.8 ms; hs 64 N = 3 (0.86 vs 0.88 ms) and head size 32 keep
-// the native plans.  One cap for both stages: attn_dq leaves each group's delta rows
-// relative to the group's first branch (-delta_0 | delta_0 - delta_i), which attn_dkdv
-// reads back group by group.
-// DTA_BWD_GROUP_MAX (A/B builds) overrides it.
-int bwd_group_cap(int dtype, int hs, int n) {
+// largest backward branch group per stage (16-bit; fp32 keeps 4).  The 3- / 4-branch
+// backward plans at head size >= 64 have no room for the paired two-waves-per-SIMD layout
+// (Q rows, K/V tiles and accumulators of 3-4 branches overflow 80 KB of LDS and 256 VGPRs)
+// and run one wave per SIMD with spills; groups of <= 2 branches recompute dP = dO V^T once
+// per group but run the paired plans.  Measured per kernel (profiles/r04_bwd_groups.json,
+// bf16, native -> groups of two): dK/dV hs 64 N = 3 0.464 -> 0.44 ms, hs 96 N = 4 11.6 ->
+// 3.4 ms, hs 128 N = 4 8.4 -> 2.9 ms; dQ hs 128 N = 4 4.0 -> 2.0 ms, but dQ at hs 64 / 96
+// N = 3 0.40 -> 0.45 / 1.69 -> 1.84 ms and hs 96 N = 4 2.27 -> 2.35 ms, so dQ groups at
+// head size 128, and at 64 for N >= 4 (0.487 either way: no re-base needed).  Head size 32
+// keeps the native plans for both.  Where the two groupings differ, the dQ stage re-bases
+// the delta rows (delta_rebase_kernel, ~3-7 us) onto the dK/dV grouping
+// (profiles/r04_bwd_rebase.json).  DTA_BWD_GROUP_MAX (A/B builds) overrides both.
+int bwd_group_cap(int dtype, int hs, int n, bool dkdv) {
 #ifdef DTA_BWD_GROUP_MAX
   return DTA_BWD_GROUP_MAX;
 #else
   if (dtype == DTA_F32) return 4;
-  return (hs >= 96 || (hs >= 64 && n >= 4)) ? 2 : 4;
+  if (dkdv) return hs >= 64 ? 2 : 4;
+  return (hs >= 128 || (hs >= 64 && hs < 96 && n >= 4)) ? 2 : 4;
 #endif
+}
+// group starts of the backward of an N-branch problem as a bit mask (bit i: a group
+// starts at branch i)
+uint64_t group_starts(int dtype, int hs, int n, int dv, int cap) {
+  uint64_t m = 0;
+  for (int g0 = 0, ng; g0 < n; g0 += ng) {
+    ng = branch_group(dtype, hs, n - g0, dv, cap);
+    m |= 1ull << g0;
+  }
+  return m;
 }
 }  // namespace dta
 
@@ -293,19 +306,28 @@ int dta_attn_bwd(const dta_attn_bwd_args* a, void* stream) {
     return q;
   };
   int e = 0;
-  const int cap = bwd_group_cap(a->dtype, p.HS, p.N);
+  // the dK/dV grouping must see delta rows encoded for its own groups (see
+  // bwd_group_cap): with dropout the rows hold delta_i itself; beyond 64 branches, or
+  // where the re-base does not apply, both stages take the dK/dV grouping
+  const int kcap = bwd_group_cap(a->dtype, p.HS, p.N, true);
+  int qcap = bwd_group_cap(a->dtype, p.HS, p.N, false);
+  if (p.drop_thr || p.N > 64) qcap = kcap;
+  const uint64_t qstarts = qcap == kcap ? 0 : group_starts(a->dtype, p.HS, p.N, p.DV, qcap);
+  const uint64_t kstarts = qcap == kcap ? 0 : group_starts(a->dtype, p.HS, p.N, p.DV, kcap);
   if (stages & DTA_BWD_DQ) {
     for (int g0 = 0, ng; g0 < p.N; g0 += ng) {
-      ng = branch_group(a->dtype, p.HS, p.N - g0, p.DV, cap);
+      ng = branch_group(a->dtype, p.HS, p.N - g0, p.DV, qcap);
       if ((e = launch_attn_dq(a->dtype, group(g0, ng), st))) return status(e);
     }
     if (p.dcoef_part &&
         (e = launch_dcoef_reduce(p.dcoef_part, p.dcoef, p.H, p.N, (int64_t)p.B * nblk, st)))
       return status(e);
+    if (qstarts != kstarts && (e = launch_delta_rebase(p.delta, rowvec, p.N, qstarts, kstarts, st)))
+      return status(e);
   }
   if (stages & DTA_BWD_DKDV) {
     for (int g0 = 0, ng; g0 < p.N; g0 += ng) {
-      ng = branch_group(a->dtype, p.HS, p.N - g0, p.DV, cap);
+      ng = branch_group(a->dtype, p.HS, p.N - g0, p.DV, kcap);
       if ((e = launch_attn_dkdv(a->dtype, group(g0, ng), st))) return status(e);
     }
   }

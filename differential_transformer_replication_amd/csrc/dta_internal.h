@@ -111,6 +111,7 @@ int launch_decode(int dtype, const DecodeParams& p, hipStream_t st);
 int launch_ln(int dtype, const LnParams& p, bool bwd, hipStream_t st);
 int launch_rope(int dtype, bool src_f32, const RopeParams& p, hipStream_t st);
 int launch_dcoef_reduce(const float* part, float* dcoef, int H, int N, int64_t per, hipStream_t st);
+int launch_delta_rebase(float* delta, int64_t rows, int N, uint64_t from, uint64_t to, hipStream_t st);
 int launch_cast(int dtype, const float* src, const T5& dst, int B, int T, int H, int N, int HS, hipStream_t st);
 
 struct SwigluParams {

@@ -641,6 +641,36 @@ int launch_dcoef_reduce(const float* part, float* dcoef, int H, int N, int64_t p
   return (int)hipGetLastError();
 }
 
+// attn_dq leaves each dQ branch group's delta rows relative to the group's first branch a
+// (-delta_a, then delta_a - delta_i); re-base them onto the dK/dV grouping (capi.hip
+// bwd_group_cap).  Bit i of from / to: a group starts at branch i.  delta is [N][rows];
+// one thread per row decodes to delta_i and re-encodes in place, in branch order.
+__global__ __launch_bounds__(256) void delta_rebase_kernel(float* delta, int64_t rows, int N,
+                                                           uint64_t from, uint64_t to) {
+  for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < rows; r += (int64_t)gridDim.x * 256) {
+    float head = 0.f;
+    for (int i = 0; i < N; ++i) {
+      float* d = delta + i * rows + r;
+      const float v = *d;
+      if ((from >> i) & 1) head = -v;
+      *d = ((from >> i) & 1) ? head : head - v;
+    }
+    for (int i = 0; i < N; ++i) {
+      float* d = delta + i * rows + r;
+      const float v = *d;
+      if ((to >> i) & 1) head = v;
+      *d = ((to >> i) & 1) ? -head : head - v;
+    }
+  }
+}
+
+int launch_delta_rebase(float* delta, int64_t rows, int N, uint64_t from, uint64_t to, hipStream_t st) {
+  const int64_t blocks = (rows + 255) / 256;
+  hipLaunchKernelGGL(delta_rebase_kernel, dim3((unsigned)(blocks < 2048 ? blocks : 2048)), dim3(256), 0, st,
+                     delta, rows, N, from, to);
+  return (int)hipGetLastError();
+}
+
 // ---- dst += (float)src (fp32 master-gradient accumulation).  HBM-bound: 8 elements
 // per thread and step (16-byte loads of 16-bit src), grid-stride, scalar tail.
 template <class E>
