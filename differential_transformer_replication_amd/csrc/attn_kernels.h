@@ -1555,436 +1555,6 @@ void attn_dq_kernel(BwdParams p) {
       }
 }
 
-// ------------------------------------- backward: dQ, two query blocks per wave ---
-// attn_dq2_kernel: the query-major backward of attn_dq_kernel re-planned for one wave per
-// SIMD.  A wave owns TWO 32-row query blocks (64 rows; the workgroup's 4 waves 256 rows)
-// and the whole 512-entry register file: the dQ accumulators of both blocks, their dO
-// rows, the dP and S' accumulators and the packed dS of every (branch, block) unit of a
-// tile.  Q_i (all branches, prescaled by sl2) sit in LDS; K_i / V tiles of 64 keys stream
-// through the LDS-DMA ring as in attn_dq_kernel.
-//
-// Per tile the work is two streams: MFMAs (per unit u = (branch, block): the seeded S'
-// chain; per block the seeded dP chain; per unit the dQ product) and VALU (per unit:
-// exp2, the dS multiply, the bf16 pack).  With no partner wave on the SIMD, the VALU of a
-// unit has to run in the gaps of MFMAs that do not depend on it.  Dq2Sched lays the tile
-// out at compile time: a fixed MFMA order (S'(u0) dP(0) S'(u1) dP(1) S'(u2) dQ(u0) S'(u3)
-// dQ(u1) ... dQ(u_last)), every LDS operand read issued R MFMAs ahead of its consumer
-// (inline asm, counted lgkmcnt), and each unit's VALU split into 16 pieces (two elements
-// each) placed earliest-deadline-first into the MFMA slots between the end of its inputs
-// and the first MFMA that needs its result or its registers.  A sched_barrier closes
-// every slot, so the compiler keeps the placement.
-#ifndef DTA_DQ2
-#define DTA_DQ2 1
-#endif
-#ifndef DTA_DQ2_R
-#define DTA_DQ2_R 2          // MFMAs of read-ahead
-#endif
-// bf16 MFMA accumulating into AGPRs (inline asm): the dQ accumulators are touched only by
-// MFMAs, so they live in the AGPR half of the register file while everything the VALU
-// reads stays in VGPRs (the unit is built with -mllvm -amdgpu-mfma-vgpr-form=1, which
-// selects VGPR accumulators for the builtins).  The hazard recognizer does not see inside
-// the asm: NOP = 1 adds the two wait states a VALU-written operand needs, and the caller
-// waits before reading the accumulators (dq2_acc_fence).
-template <bool NOP>
-__device__ __forceinline__ void mfma_agpr(f32x16& acc, bf16x8 a, bf16x8 b) {
-  if constexpr (NOP) asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
-  else asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
-}
-// The compiler also does not see that an asm MFMA is still reading its A / B VGPRs after it
-// issues: it may hand them to the next VALU result at once (a first attn_fwd3 build wrote a
-// branch condition into a V fragment one instruction after the MFMA that read it).  Every
-// asm MFMA of a stream therefore keeps the previous one's operands alive until it has
-// itself issued; mfma_release after the stream's fence ends the last pair.
-struct MfmaHold { bf16x8 a, b; };
-template <bool NOP>
-__device__ __forceinline__ void mfma_agpr(f32x16& acc, bf16x8 a, bf16x8 b, MfmaHold& h) {
-  mfma_agpr<NOP>(acc, a, b);
-  asm volatile("" ::"v"(h.a), "v"(h.b));
-  h.a = a;
-  h.b = b;
-}
-__device__ __forceinline__ void mfma_release(const MfmaHold& h) { asm volatile("" ::"v"(h.a), "v"(h.b)); }
-__device__ __forceinline__ void dq2_acc_fence() { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory"); }
-// pin accumulators after a fence: their readers (v_accvgpr_read, allocator copies) then
-// depend on the pins, which volatile ordering keeps after the fence's wait states
-__device__ __forceinline__ void acc_pin(f32x16& a) { asm volatile("" : "+a"(a)); }
-template <class A, int M>
-__device__ __forceinline__ void acc_pin(A (&a)[M]) {
-#pragma unroll
-  for (int i = 0; i < M; ++i) acc_pin(a[i]);
-}
-
-namespace dq2 {
-enum : int { SS = 0, SC = 1, DS = 2, DC = 3, CC = 4 };
-struct Op { int kind = 0, u = 0, qb = 0, i = 0, a = 0, b = 0, c = 0; };
-constexpr int PIECES = 16;     // VALU pieces per unit: 2 key blocks x 16 elements, two at a time
-
-template <int N, int NSQ, int NSV, int NHB>
-struct Sched {
-  static constexpr int NKB = 2, U = 2 * N, SR = 2;            // S' accumulator sets in flight
-  static constexpr int NS1 = NKB + NSQ * NKB, ND1 = NKB + NSV * NKB, NC1 = NHB * NKB * 2;
-  static constexpr int NOPS = U * NS1 + 2 * ND1 + U * NC1;
-  // unit u -> branch (highest first: branch 0's VALU, without the delta add, is the lightest) and block
-  static constexpr int ui(int u) { return N - 1 - u / 2; }
-  static constexpr int uq(int u) { return u % 2; }
-  Op ops[NOPS];
-  int s0[U] = {}, s1[U] = {}, c0[U] = {}, d1[2] = {};
-  int E[U] = {}, Dl[U] = {};
-  int pslot[U][PIECES] = {};
-  int npiece[NOPS] = {};       // VALU pieces in slot s
-  int pu[NOPS][PIECES] = {};   // ... which (unit, piece): u * PIECES + j
-  int nreads[NOPS] = {};       // LDS read instructions op s issues (at slot s - R)
-  int rid[NOPS] = {};          // index of op s's b128 read among all b128 reads (K / V / Q frags)
-  int qid[NOPS] = {};          // Q fragment read index (S' ops with b == 0)
-  int tid[NOPS] = {};          // tr block index (dQ ops with c == 0)
-  bool ok = true;
-  constexpr void add_s(int& n, int u) {
-    s0[u] = n;
-    for (int kb = 0; kb < NKB; ++kb) { ops[n].kind = SS; ops[n].u = u; ops[n].qb = uq(u); ops[n].i = ui(u); ops[n].b = kb; ++n; }
-    for (int st = 0; st < NSQ; ++st)
-      for (int kb = 0; kb < NKB; ++kb) {
-        ops[n].kind = SC; ops[n].u = u; ops[n].qb = uq(u); ops[n].i = ui(u); ops[n].a = st; ops[n].b = kb; ++n;
-      }
-    s1[u] = n - 1;
-  }
-  constexpr void add_d(int& n, int qb) {
-    for (int kb = 0; kb < NKB; ++kb) { ops[n].kind = DS; ops[n].qb = qb; ops[n].b = kb; ++n; }
-    for (int s = 0; s < NSV; ++s)
-      for (int kb = 0; kb < NKB; ++kb) { ops[n].kind = DC; ops[n].qb = qb; ops[n].a = s; ops[n].b = kb; ++n; }
-    d1[qb] = n - 1;
-  }
-  constexpr void add_c(int& n, int u) {
-    c0[u] = n;
-    for (int d = 0; d < NHB; ++d)
-      for (int kb = 0; kb < NKB; ++kb)
-        for (int ks = 0; ks < 2; ++ks) {
-          ops[n].kind = CC; ops[n].u = u; ops[n].qb = uq(u); ops[n].i = ui(u); ops[n].a = d; ops[n].b = kb; ops[n].c = ks; ++n;
-        }
-  }
-  constexpr Sched() {
-    int n = 0;
-    add_s(n, 0); add_d(n, 0);
-    if (U > 1) { add_s(n, 1); add_d(n, 1); }
-    for (int u = 2; u < U; ++u) { add_s(n, u); add_c(n, u - 2); }
-    for (int u = (U > 2 ? U - 2 : 0); u < U; ++u) add_c(n, u);
-    if (n != NOPS) ok = false;
-    // VALU windows: after the unit's S' and dP chains, before its dQ product and before the
-    // S' chain that reuses its accumulator set
-    for (int u = 0; u < U; ++u) {
-      E[u] = (s1[u] > d1[uq(u)] ? s1[u] : d1[uq(u)]) + 1;
-      Dl[u] = c0[u] - 1;       // the last pack at least one MFMA before its dQ product
-      if (u + SR < U && s0[u + SR] < Dl[u]) Dl[u] = s0[u + SR];
-    }
-    // each unit's pieces in order over its window, up to the lowest per-slot cap that fits
-    int load[NOPS] = {};
-    for (int u = 0; u < U; ++u) {
-      int cap = 1;
-      for (;; ++cap) {
-        int room = 0;
-        for (int x = E[u]; x < Dl[u]; ++x) room += load[x] < cap ? cap - load[x] : 0;
-        if (room >= PIECES || cap >= PIECES) break;
-      }
-      int j = 0;
-      for (int x = E[u]; x < Dl[u] && j < PIECES; ++x)
-        while (load[x] < cap && j < PIECES) {
-          pslot[u][j] = x;
-          if (npiece[x] < PIECES) pu[x][npiece[x]++] = u * PIECES + j; else ok = false;
-          ++load[x];
-          ++j;
-        }
-      if (j < PIECES) ok = false;
-    }
-    int nb = 0, nq = 0, ntr = 0;
-    for (int s = 0; s < NOPS; ++s) {
-      const Op& o = ops[s];
-      if (o.kind == SC) {
-        rid[s] = nb++; nreads[s] = 1;
-        if (o.b == 0) { qid[s] = nq++; nreads[s] = 2; }
-      } else if (o.kind == DC) {
-        rid[s] = nb++; nreads[s] = 1;
-      } else if (o.kind == CC && o.c == 0) {
-        tid[s] = ntr++; nreads[s] = 4;
-      }
-    }
-  }
-  // LDS read instructions issued for ops (s, s + R]: lgkmcnt at op s
-  constexpr int pending(int s, int R) const {
-    int c = 0;
-    for (int x = s + 1; x <= s + R && x < NOPS; ++x) c += nreads[x];
-    return c;
-  }
-};
-template <int N, int NSQ, int NSV, int NHB>
-struct Hold { static constexpr Sched<N, NSQ, NSV, NHB> v{}; };
-}  // namespace dq2
-
-template <class E, int HS, int N, int DV>
-struct Dq2Cfg {
-  static constexpr int NW = 4, BM = 256, BN = 64;
-  static constexpr int nQ = N * BM * HS, nK = N * BN * HS, nV = BN * DV;
-  static constexpr int NS = ring_stages(nQ * (int)sizeof(E), (nK + nV) * (int)sizeof(E));
-  static constexpr int bytes = (nQ + NS * (nK + nV)) * (int)sizeof(E);
-  static constexpr int NHB = HS / 32;
-  // per-lane registers: dQ accumulators, dO rows, dP, two S' sets, packed dS of every
-  // unit, seeds, read buffers and addresses
-  static constexpr int regs = 2 * N * NHB * 16 + 2 * DV / 4 + 2 * 2 * 16 + 2 * 2 * 16 + 2 * N * 16 + 8 * N + 92;
-  static constexpr bool shape_ok = DTA_DQ2 && std::is_same<E, __bf16>::value && (HS == 32 || HS == 64 || HS == 128) &&
-                                   (DV == HS || DV == 2 * HS) && DV <= 128 && bytes <= 160 * 1024 && regs <= 512;
-  template <bool S, int = 0> struct Sok { static constexpr bool v = false; };
-  template <int X> struct Sok<true, X> { static constexpr bool v = dq2::Hold<N, HS / 16, DV / 16, HS / 32>::v.ok; };
-  static constexpr bool ok = Sok<shape_ok>::v;
-};
-
-template <class E, int HS, int N, int DV>
-__global__ __launch_bounds__(256, 1)
-void attn_dq2_kernel(BwdParams p) {
-  using O = Ops<E>;
-  using frag = typename O::frag;
-  using CF = Dq2Cfg<E, HS, N, DV>;
-  constexpr int NW = CF::NW, BM = CF::BM, BN = CF::BN, NTHR = NW * 64, KS = O::KSTEP;
-  constexpr int NSQ = HS / KS, NSV = DV / KS, NHB = HS / 32, NKB = 2, NS = CF::NS;
-  constexpr int ROWB = HS * (int)sizeof(E), VROWB = DV * (int)sizeof(E);
-  constexpr int R = DTA_DQ2_R;
-  using SCH = dq2::Hold<N, NSQ, NSV, NHB>;
-  constexpr int NOPS = dq2::Sched<N, NSQ, NSV, NHB>::NOPS;
-  constexpr int U = 2 * N;
-  static_assert(SCH::v.ok, "dQ2 schedule");
-
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  E* Qs = reinterpret_cast<E*>(smem);   // [N][BM][HS], prescaled by sl2
-  E* Kb = Qs + CF::nQ;                  // [NS][N][BN][HS]
-  E* Vb = Kb + NS * CF::nK;             // [NS][BN][DV]
-
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  int tid = threadIdx.x, lane = tid & 63;
-  int hf = lane >> 5, c32 = lane & 31;
-  int bx, by, bz, lin;
-  lpt_order(bx, by, bz, lin);
-  const int qt = gridDim.x - 1 - bx;
-  const int hh = by, b = bz;
-  const int T = p.T;
-  const int q0 = qt * BM, qw0 = q0 + wave * 64;
-
-  const E* gq = reinterpret_cast<const E*>(p.q.p) + b * p.q.sb + hh * p.q.sh;
-  const E* gk = reinterpret_cast<const E*>(p.k.p) + b * p.k.sb + hh * p.k.sh;
-  const E* gv = reinterpret_cast<const E*>(p.v.p) + b * p.v.sb + hh * p.v.sh;
-  const E* gdo = reinterpret_cast<const E*>(p.dout.p) + b * p.dout.sb + hh * p.dout.sh;
-  const int64_t gob = b * p.obr.sb + hh * p.obr.sh;
-  const int kend = min(T, q0 + BM);
-  const int ntiles = (kend + BN - 1) / BN;
-  using KR = KvRing<E, HS, N, DV, BN, NW>;
-  uint32_t doff[KR::MYP];
-  KR::offsets(p.k.st, p.k.si, p.v.st, wave, lane, doff);
-  // past the last tile a null tile (no rows: zeros into a free slot): no branch in the
-  // stream, constant vmcnt waits
-  auto stage_kv = [&](int kt, int buf) {
-    KR::issue_pre(gk, p.k.st, gv, p.v.st, kt * BN, kt < ntiles ? T : 0, Kb + buf * CF::nK, Vb + buf * CF::nV, wave, doff);
-  };
-
-  // ---- per-block row operands: dO rows (B operands of dP), delta, LSE seeds
-  frag df[2][NSV];
-  frag f_one = O::zero(), f_lse[2][N], f_dp[2];
-  float coef[N], dd[2][N];
-  const int64_t bstride = (int64_t)p.B * p.H * T;
-#pragma unroll
-  for (int i = 0; i < N; ++i) coef[i] = p.coef[hh * p.cst + i];
-  if (hf == 0) { f_one[0] = (E)1.f; f_one[1] = (E)1.f; }
-#pragma unroll
-  for (int qb = 0; qb < 2; ++qb) {
-    const int qrow = qw0 + 32 * qb + c32;
-    const bool rowok = qrow < T;
-    const int64_t rs = ((int64_t)b * p.H + hh) * T + qrow;
-#pragma unroll
-    for (int s = 0; s < NSV; ++s)
-      df[qb][s] = rowok ? O::load_global(gdo + (int64_t)qrow * p.dout.st + s * KS + hf * O::KH) : O::zero();
-    float del0 = 0.f;
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-      const float lse = rowok ? p.lse[rs + i * bstride] : 0.f;
-      float d = 0.f;
-      if (rowok) {
-#pragma unroll
-        for (int s = 0; s < NSV; ++s) {
-          float ov[8];
-          load_ob8(p.obr.p, gob + (int64_t)qrow * p.obr.st + i * p.obr.si + s * KS + hf * O::KH, p.ob16, ov);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) d = fmaf((float)df[qb][s][j], ov[j], d);
-        }
-      }
-      d = wave_sum_halves(d);
-      if (i == 0) del0 = d;
-      dd[qb][i] = del0 - d;
-      f_lse[qb][i] = seed_frag<E>(lse, hf);
-      if (rowok && hf == 0) p.delta[rs + i * bstride] = i == 0 ? -d : del0 - d;
-      float w = (rowok && hf == 0) ? d : 0.f;
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) w += __shfl_xor(w, o, 64);
-      const int blk = qw0 + 32 * qb;
-      if (p.dcoef_part) {
-        if (lane == 0 && blk < T) p.dcoef_part[(((int64_t)hh * p.cst + i) * p.B + b) * ((T + 31) / 32) + blk / 32] = w;
-      } else if (lane == 0 && blk < T) {
-        atomicAdd(p.dcoef + hh * p.cst + i, w);
-      }
-    }
-    f_dp[qb] = seed_frag<E>(-del0, hf);
-  }
-  // loop-invariant MFMA operands (the dO rows, the seed fragments) pinned to AGPRs: MFMAs
-  // read A / B operands from either half, and the VGPRs go to the values the VALU touches
-#pragma unroll
-  for (int qb = 0; qb < 2; ++qb) {
-#pragma unroll
-    for (int s = 0; s < NSV; ++s) asm volatile("" : "+a"(df[qb][s]));
-#pragma unroll
-    for (int i = 0; i < N; ++i) asm volatile("" : "+a"(f_lse[qb][i]));
-    asm volatile("" : "+a"(f_dp[qb]));
-  }
-
-#pragma unroll
-  for (int i = 0; i < N; ++i) stage<E, HS, BM, HS, NTHR>(Qs + i * BM * HS, gq + i * p.q.si, p.q.st, q0, T - 1, tid);
-  const int tile_pieces = KR::pieces(wave);
-  for (int j = 0; j < NS - 1; ++j) stage_kv(j, j);
-  wait_vm(tile_pieces * (NS - 2));
-  lds_barrier();
-  scale_lds<E, NTHR>(Qs, CF::nQ, p.sl2, tid);
-  lds_barrier();
-
-  f32x16 dq[2][N][NHB];
-  MfmaHold hold{};
-#pragma unroll
-  for (int qb = 0; qb < 2; ++qb)
-#pragma unroll
-    for (int i = 0; i < N; ++i)
-#pragma unroll
-      for (int d = 0; d < NHB; ++d) dq[qb][i][d] = f32x16{};
-
-  int LrV = row_lane<VROWB>(lane), LrK = row_lane<ROWB>(lane), LtK = tr_lane<ROWB>(lane);
-
-  // one tile: the MFMA stream with the VALU pieces in its slots
-  auto body = [&](int kt, auto MASKED, int kt_dma) {
-    constexpr bool MASK = decltype(MASKED)::value;
-    asm volatile("" : "+v"(LrV), "+v"(LrK), "+v"(LtK));
-    // the seed MFMAs are loop-invariant: keep them in the tile (an opaque "ones" operand),
-    // or the compiler hoists their results and copies 16 registers back per use
-    frag one = f_one;
-    asm volatile("" : "+v"(one));
-    const int buf = kt % NS, k0 = kt * BN;
-    const unsigned kbase = lds_addr(Kb + buf * CF::nK), vbase = lds_addr(Vb + buf * CF::nV);
-    const unsigned bK = LrK + kbase, tK = LtK + kbase, bV = LrV + vbase;
-    const unsigned bQ = LrK + lds_addr(Qs) + wave * 64 * ROWB;
-    int lim[2];
-#pragma unroll
-    for (int qb = 0; qb < 2; ++qb) lim[qb] = min(qw0 + 32 * qb + (lane & 31), T - 1) - k0 - 4 * (lane >> 5);
-    f32x16 dp[2][NKB], sa[2][NKB];
-    frag pk[U][NKB * 2];
-    constexpr int RBN = R + 3, RQN = R / 2 + 2, RTN = R / 2 + 2;
-    i32x4 rb[RBN], rq[RQN];
-    lds64 rt[RTN][4];
-    auto issue = [&](auto S_) {
-      constexpr int s = decltype(S_)::value;
-      constexpr dq2::Op o = SCH::v.ops[s];
-      if constexpr (o.kind == dq2::SC) {
-        ds128<o.i * BN * ROWB + o.b * 32 * ROWB>(rb[SCH::v.rid[s] % RBN], bK ^ (32 * o.a));
-        if constexpr (o.b == 0) ds128<o.i * BM * ROWB + o.qb * 32 * ROWB>(rq[SCH::v.qid[s] % RQN], bQ ^ (32 * o.a));
-      } else if constexpr (o.kind == dq2::DC) {
-        ds128<o.b * 32 * VROWB>(rb[SCH::v.rid[s] % RBN], bV ^ (32 * o.a));
-      } else if constexpr (o.kind == dq2::CC && o.c == 0) {
-        tr_issue<ROWB, 32 * o.b, o.i * BN * ROWB>(rt[SCH::v.tid[s] % RTN], tK ^ (64 * o.a), tK ^ (64 * o.a + 32));
-      }
-    };
-    auto piece = [&](auto PU) {
-      constexpr int u = decltype(PU)::value / dq2::PIECES, j = decltype(PU)::value % dq2::PIECES;
-      constexpr int i = dq2::Sched<N, NSQ, NSV, NHB>::ui(u), qb = dq2::Sched<N, NSQ, NSV, NHB>::uq(u);
-      constexpr int kb = j / 8, r0 = (j % 8) * 2, sr = u % 2;
-#pragma unroll
-      for (int r = r0; r < r0 + 2; ++r) {
-        float arg = sa[sr][kb][r];
-        if constexpr (MASK) arg = (kb * 32 + (r & 3) + 8 * (r >> 2) > lim[qb]) ? -INFINITY : arg;
-        const float pr = exp2_fast(arg);
-        sa[sr][kb][r] = i == 0 ? pr * dp[qb][kb][r] : pr * (dp[qb][kb][r] + dd[qb][i]);
-      }
-      if constexpr (j % 4 == 3) pk[u][kb * 2 + (j % 8) / 4] = O::template pack<(j % 8) / 4>(sa[sr][kb]);
-    };
-    sfor<(R < NOPS ? R : NOPS)>([&](auto S_) { issue(S_); });
-    sfor<NOPS>([&](auto S_) {
-      constexpr int s = decltype(S_)::value;
-      constexpr dq2::Op o = SCH::v.ops[s];
-      if constexpr (s + R < NOPS) issue(std::integral_constant<int, s + R>{});
-      // this wave's LDS-DMA pieces of tile kt_dma, spread over the stream
-      sfor<KR::MYP>([&](auto U) {
-        constexpr int u = decltype(U)::value;
-        if constexpr (s == (u + 1) * NOPS / (KR::MYP + 1))
-          KR::template issue_one<u>(gk, p.k.st, gv, p.v.st, kt_dma * BN, kt_dma < ntiles ? T : 0,
-                                    Kb + (kt_dma % NS) * CF::nK, Vb + (kt_dma % NS) * CF::nV, wave, doff[u]);
-      });
-      if constexpr (SCH::v.nreads[s] > 0) lgkm_wait<SCH::v.pending(s, R)>();
-      if constexpr (o.kind == dq2::SS) {
-        sa[o.u % 2][o.b] = O::mma(one, f_lse[o.qb][o.i], f32x16{});
-      } else if constexpr (o.kind == dq2::SC) {
-        i32x4& kr = rb[SCH::v.rid[s] % RBN];
-        i32x4& qr = rq[(o.b == 0 ? SCH::v.qid[s] : SCH::v.qid[s - 1]) % RQN];
-        asm volatile("" : "+v"(kr), "+v"(qr));
-        sa[o.u % 2][o.b] = O::mma(__builtin_bit_cast(frag, kr), __builtin_bit_cast(frag, qr), sa[o.u % 2][o.b]);
-      } else if constexpr (o.kind == dq2::DS) {
-        dp[o.qb][o.b] = O::mma(one, f_dp[o.qb], f32x16{});
-      } else if constexpr (o.kind == dq2::DC) {
-        i32x4& vr = rb[SCH::v.rid[s] % RBN];
-        asm volatile("" : "+v"(vr));
-        dp[o.qb][o.b] = O::mma(__builtin_bit_cast(frag, vr), df[o.qb][o.a], dp[o.qb][o.b]);
-      } else {
-        lds64 (&tr)[4] = rt[(o.c == 0 ? SCH::v.tid[s] : SCH::v.tid[s - 1]) % RTN];
-        if constexpr (o.c == 0) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(tr[j]));
-        }
-        mfma_agpr<(s == SCH::v.c0[o.u])>(dq[o.qb][o.i][o.a], tr_frag<E>(tr, o.c), pk[o.u][o.b * 2 + o.c], hold);
-      }
-      sfor<SCH::v.npiece[s]>([&](auto K) { piece(std::integral_constant<int, SCH::v.pu[s][decltype(K)::value]>{}); });
-      __builtin_amdgcn_sched_barrier(0);
-    });
-  };
-  auto step = [&](int kt, auto MASKED, bool live) {
-    if (live) body(kt, MASKED, kt + NS - 1);
-    else stage_kv(kt + NS - 1, (kt + NS - 1) % NS);
-    wait_vm(tile_pieces * (NS - 2));
-    lds_barrier();
-  };
-  // per wave: tiles wholly below its first row, its diagonal / ragged tiles, then tiles past
-  // its last row (DMA share and barrier only)
-  const bool wave_live = qw0 < T;
-  const int nfull = wave_live ? min(ntiles, min(qw0 / BN, T / BN)) : 0;
-  const int nlive = wave_live ? min(ntiles, qw0 / BN + 1) : 0;
-  for (int kt = 0; kt < nfull; ++kt) step(kt, std::false_type{}, true);
-  for (int kt = nfull; kt < nlive; ++kt) step(kt, std::true_type{}, true);
-  for (int kt = nlive; kt < ntiles; ++kt) step(kt, std::false_type{}, false);
-  dq2_acc_fence();
-  acc_pin(dq);
-  mfma_release(hold);
-
-#pragma unroll
-  for (int qb = 0; qb < 2; ++qb) {
-    const int qrow = qw0 + 32 * qb + c32;
-    if (qrow >= T) continue;
-#pragma unroll
-    for (int i = 0; i < N; ++i)
-#pragma unroll
-      for (int d = 0; d < NHB; ++d)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int e = d * 32 + 8 * g + 4 * hf;
-          const float sc = p.scale * coef[i];
-          float a0 = dq[qb][i][d][4 * g] * sc, a1 = dq[qb][i][d][4 * g + 1] * sc;
-          float a2 = dq[qb][i][d][4 * g + 2] * sc, a3 = dq[qb][i][d][4 * g + 3] * sc;
-          if (p.rope) rope_inv4(p.rope, qrow, HS, e, a0, a1, a2, a3);
-          if (p.dq32) {
-            store4<float>(p.dq32 + ((((int64_t)b * T + qrow) * p.H + hh) * p.cst + i) * HS + e, a0, a1, a2, a3);
-          } else {
-            E* gdq = reinterpret_cast<E*>(p.dq.p) + b * p.dq.sb + (int64_t)qrow * p.dq.st + hh * p.dq.sh + i * p.dq.si;
-            store4<E>(gdq + e, a0, a1, a2, a3);
-          }
-        }
-  }
-}
-
 // One query tile of the key-major backward -- Q_i rows, dO rows, LSE rows and
 // (with DELTA) c*delta rows -- streamed into one ring stage by buffer_load ... lds.
 // Stage layout: [N][BQ][HSP] Q image | [BQ][DVP] dO image | [NP] lse | [NP] c*delta
@@ -2498,820 +2068,6 @@ void attn_dkdv_kernel(BwdParams p) {
   }
 }
 
-// ------------------------------- forward: key tiles software-pipelined ---
-// attn_fwd3_kernel: the fixed-reference-maximum forward (FAST, as attn_fwd) for one wave per
-// SIMD with the key-tile loop software-pipelined, so the matrix pipe always has work that
-// does not wait on the softmax: in iteration j a wave issues the O_i^T += V^T P^T products of
-// tile j-1 and the S_i^T chains of tile j+1 while its VALU turns tile j's scores into P
-// (exp2 against the fixed row maxima, row sums, bf16 packs).  4 waves x 32 query rows; Q_i
-// rows and the O_i^T accumulators in AGPRs; K_i / V tiles of 64 keys through a 5-stage
-// LDS-DMA ring (tile j+3 issued in iteration j into the slot tile j-2 left).  The first tile
-// sets the row maxima (per-tile max); a workgroup whose P could leave the operand range
-// re-runs with exact maxima from a pass of S^T over its tiles (every P <= 1).
-namespace fw3 {
-enum : int { SC = 0, PV = 1 };
-struct Op { int kind = 0, i = 0, a = 0, b = 0, c = 0; };   // SC: a st, b kb; PV: a d, b kb, c ks
-// Per branch i: the products of tile j-1 (PV(i), reading pk[i]) and then the S^T chain of
-// tile j+1 (S(i), writing the free S buffer).  Branch i's VALU pieces (P of tile j from the
-// current S buffer) are spread over S(i-1) and PV(i); its packs into pk[i] sit right after
-// PV(i) (before S(i)'s first MFMA), so the current and the next S buffer of a branch are
-// never live together: 1.5 tiles of scores per branch instead of 2.
-template <int N, int NSQ, int NDB, bool HAS_S, bool HAS_V>
-struct Sched {
-  static constexpr int NKB = 2, PIECES = 16;                 // VALU pieces per branch (element pairs)
-  static constexpr int NS1 = HAS_S ? NSQ * NKB : 0, NP1 = NDB * NKB * 2;
-  static constexpr int NOPS = N * (NS1 + NP1), NP = HAS_V ? N * PIECES : 0;
-  Op ops[NOPS];
-  int nreads[NOPS] = {}, rid[NOPS] = {}, tid[NOPS] = {};
-  int npiece[NOPS + 1] = {}, pp[NOPS + 1][8] = {};
-  int npack[NOPS + 1] = {}, pkk[NOPS + 1][8] = {};          // packs done BEFORE the slot's MFMA; NOPS = after the stream
-  bool ok = true;
-  constexpr Sched() {
-    int n = 0;
-    for (int i = 0; i < N; ++i) {
-      const int w0 = i == 0 ? 0 : n - NS1;                  // branch i's piece window: S(i-1), PV(i)
-      for (int d = 0; d < NDB; ++d)
-        for (int kb = 0; kb < NKB; ++kb)
-          for (int ks = 0; ks < 2; ++ks) {
-            ops[n].kind = PV; ops[n].i = i; ops[n].a = d; ops[n].b = kb; ops[n].c = ks;
-            ++n;
-          }
-      const int w1 = n;
-      if (HAS_V) {
-        for (int j = 0; j < PIECES; ++j) {
-          const int s = w0 + j * (w1 - w0) / PIECES;
-          if (npiece[s] < 8) pp[s][npiece[s]++] = i * PIECES + j; else ok = false;
-        }
-        for (int x = 0; x < 4; ++x) {
-          if (npack[n] < 8) pkk[n][npack[n]++] = i * 4 + x; else ok = false;
-        }
-      }
-      if (HAS_S)
-        for (int st = 0; st < NSQ; ++st)
-          for (int kb = 0; kb < NKB; ++kb) { ops[n].kind = SC; ops[n].i = i; ops[n].a = st; ops[n].b = kb; ++n; }
-    }
-    if (n != NOPS) ok = false;
-    int nb = 0, ntr = 0;
-    for (int s = 0; s < NOPS; ++s) {
-      if (ops[s].kind == SC) { rid[s] = nb++; nreads[s] = 1; }
-      else if (ops[s].c == 0) { tid[s] = ntr++; nreads[s] = 4; }
-    }
-  }
-  constexpr int pending(int s, int R) const {
-    int c = 0;
-    for (int x = s + 1; x <= s + R && x < NOPS; ++x) c += nreads[x];
-    return c;
-  }
-};
-template <int N, int NSQ, int NDB, bool HAS_S, bool HAS_V>
-struct Hold { static constexpr Sched<N, NSQ, NDB, HAS_S, HAS_V> v{}; };
-}  // namespace fw3
-
-#ifndef DTA_FWD3
-#define DTA_FWD3 1
-#endif
-#ifndef DTA_FWD3_SPREAD
-#define DTA_FWD3_SPREAD 1      // LDS-DMA pieces spread over the stream (0: one burst per tile)
-#endif
-template <class E, int HS, int N, int DV>
-struct Fw3Cfg {
-  static constexpr int NW = 4, BM = 128, BN = 64, NS = 5;
-  static constexpr int nK = N * BN * HS, nV = BN * DV;
-  static constexpr int bytes = NS * (nK + nV) * (int)sizeof(E);
-  static constexpr int aregs = N * (DV / 32) * 16 + N * HS / 4;       // O_i^T, Q_i rows
-  static constexpr int vregs = 2 * N * 2 * 16 + N * 16 + 90;          // S^T (two tiles), packs, the rest
-  static constexpr bool shape_ok = DTA_FWD3 && std::is_same<E, __bf16>::value && (HS == 32 || HS == 64 || HS == 128) &&
-                                   (DV == 2 * HS || (N == 1 && DV == HS)) && N <= 2 && aregs <= 240 && vregs <= 250 &&
-                                   bytes <= 160 * 1024 && KvRing<E, HS, N, DV, BN, NW>::ok;
-  template <bool S, int = 0> struct Sok { static constexpr bool v = false; };
-  template <int X> struct Sok<true, X> {
-    static constexpr bool v = fw3::Hold<N, HS / 16, DV / 32, true, true>::v.ok && fw3::Hold<N, HS / 16, DV / 32, false, true>::v.ok &&
-                              fw3::Hold<N, HS / 16, DV / 32, false, false>::v.ok;
-  };
-  static constexpr bool ok = Sok<shape_ok>::v;
-};
-
-template <class E, int HS, int N, int DV>
-__global__ __launch_bounds__(256, 1)
-void attn_fwd3_kernel(FwdParams p) {
-  using O = Ops<E>;
-  using frag = typename O::frag;
-  using CF = Fw3Cfg<E, HS, N, DV>;
-  constexpr int NW = CF::NW, BM = CF::BM, BN = CF::BN, KS = O::KSTEP, NS = CF::NS;
-  constexpr int NSQ = HS / KS, NDB = DV / 32, NKB = 2;
-  constexpr int ROWB = HS * (int)sizeof(E), VROWB = DV * (int)sizeof(E);
-  constexpr int R = DTA_DQ2_R;
-  constexpr float LSMAX = std::is_same<E, _Float16>::value ? 0x1p15f : 0x1p60f;
-
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  E* Kb = reinterpret_cast<E*>(smem);    // [NS][N][BN][HS]
-  E* Vb = Kb + NS * CF::nK;              // [NS][BN][DV]
-
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  int tid = threadIdx.x, lane = tid & 63;
-  int hf = lane >> 5, c32 = lane & 31;
-  int bx, by, bz, lin;
-  lpt_order(bx, by, bz, lin);
-  const int qt = gridDim.x - 1 - bx;
-  // branch-split launch (N == 1 instantiation, p.bsplit branches per head, as attn_fwd):
-  // workgroup (head, branch br) writes O_br and LSE_br; a combine pass forms O
-  const int nsp = (N == 1 && p.bsplit > 1) ? p.bsplit : 1;
-  const int hh = by / nsp, br = by - hh * nsp, b = bz;
-  const int T = p.T;
-  const int q0 = qt * BM, qw0 = q0 + wave * 32;
-  const int qrow = qw0 + c32;
-  const E* gq = reinterpret_cast<const E*>(p.q.p) + b * p.q.sb + hh * p.q.sh + br * p.q.si;
-  const E* gk = reinterpret_cast<const E*>(p.k.p) + b * p.k.sb + hh * p.k.sh + br * p.k.si;
-  const E* gv = reinterpret_cast<const E*>(p.v.p) + b * p.v.sb + hh * p.v.sh;
-  const int kend = min(T, q0 + BM);
-  const int ntiles = (kend + BN - 1) / BN;
-  using KR = KvRing<E, HS, N, DV, BN, NW>;
-  uint32_t doff[KR::MYP];
-  KR::offsets(p.k.st, p.k.si, p.v.st, wave, lane, doff);
-  // every iteration issues one tile: past the last one a null tile (no rows: the DMA reads
-  // nothing and writes zeros into a free slot), so the stream carries no branch and every
-  // vmcnt is a constant
-  auto stage_kv = [&](int kt) {
-    KR::issue_pre(gk, p.k.st, gv, p.v.st, kt * BN, kt < ntiles ? T : 0, Kb + (kt % NS) * CF::nK, Vb + (kt % NS) * CF::nV,
-                  wave, doff);
-  };
-  const int tile_pieces = KR::pieces(wave);
-  // vmcnt such that tile `need` has landed when every tile up to `issued` was issued
-  auto wait_tiles = [&](int need, int issued) { wait_vm(tile_pieces * (issued - need)); };
-
-  // this wave's Q_i rows: B operands of S^T = K_i Q_i^T, in AGPRs
-  frag qf[N][NSQ];
-#pragma unroll
-  for (int i = 0; i < N; ++i)
-#pragma unroll
-    for (int s = 0; s < NSQ; ++s) {
-      qf[i][s] = qrow < T ? O::load_global(gq + (int64_t)qrow * p.q.st + i * p.q.si + s * KS + hf * O::KH) : O::zero();
-      asm volatile("" : "+a"(qf[i][s]));
-    }
-  f32x16 acc[N][NDB];
-  MfmaHold hold{};
-  float m[N], l[N];
-  float bad = 0.f;
-  const bool wave_live = qw0 < T;
-  const int nlive = wave_live ? min(ntiles, (qw0 + 31) / BN + 1) : 0;
-  const int nfull = wave_live ? min(nlive, min(qw0 / BN, T / BN)) : 0;
-  int LrK = row_lane<ROWB>(lane), LtV = tr_lane<VROWB>(lane);
-  f32x16 sa[2][N][NKB];
-  frag pk[N][NKB * 2];
-
-  auto mask_tile = [&](int kt, f32x16 (&s)[N][NKB]) {
-    const int lim = min(qrow, T - 1) - kt * BN - 4 * hf;
-#pragma unroll
-    for (int i = 0; i < N; ++i)
-#pragma unroll
-      for (int kb = 0; kb < NKB; ++kb)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) s[i][kb][r] = (kb * 32 + (r & 3) + 8 * (r >> 2) > lim) ? -INFINITY : s[i][kb][r];
-  };
-  // S^T of tile kt, straight code (prologue, max pre-pass)
-  auto s_tile = [&](int kt, f32x16 (&s)[N][NKB]) {
-    const unsigned bK = LrK + lds_addr(Kb + (kt % NS) * CF::nK);
-    sfor<N>([&](auto I) {
-      constexpr int i = decltype(I)::value;
-#pragma unroll
-      for (int kb = 0; kb < NKB; ++kb) s[i][kb] = f32x16{};
-      sfor<NSQ>([&](auto ST) {
-        constexpr int st = decltype(ST)::value;
-        i32x4 k0v, k1v;
-        ds128<i * BN * ROWB>(k0v, bK ^ (32 * st));
-        ds128<i * BN * ROWB + 32 * ROWB>(k1v, bK ^ (32 * st));
-        lgkm_wait<0>();
-        asm volatile("" : "+v"(k0v), "+v"(k1v));
-        s[i][0] = O::mma(__builtin_bit_cast(frag, k0v), qf[i][st], s[i][0]);
-        s[i][1] = O::mma(__builtin_bit_cast(frag, k1v), qf[i][st], s[i][1]);
-      });
-    });
-  };
-  // P of tile kt in place, row sums, packs (straight code: the first tile)
-  auto p_tile = [&](f32x16 (&s)[N][NKB]) {
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-      float ls = 0.f;
-#pragma unroll
-      for (int kb = 0; kb < NKB; ++kb) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          s[i][kb][r] = exp2_fast(fmaf(s[i][kb][r], p.sl2, -m[i]));
-          ls += s[i][kb][r];
-        }
-        pk[i][kb * 2 + 0] = O::template pack<0>(s[i][kb]);
-        pk[i][kb * 2 + 1] = O::template pack<1>(s[i][kb]);
-      }
-      l[i] += ls;
-      bad = (ls <= LSMAX) ? bad : 1.f;
-    }
-  };
-  // one pipelined iteration: O += V^T P^T of tile j-1 (HAS_V: and P of tile j from sa[CUR];
-  // HAS_S: S^T of tile j+1 into sa[1 - CUR])
-  auto iter = [&](int j, auto HASS, auto HASV, auto MASKED, auto CURB, int kt_dma) {
-    constexpr bool HAS_S = decltype(HASS)::value, HAS_V = decltype(HASV)::value, MASK = decltype(MASKED)::value;
-    constexpr int CUR = decltype(CURB)::value, NXT = 1 - CUR;
-    using SCH = fw3::Hold<N, NSQ, NDB, HAS_S, HAS_V>;
-    using SD = fw3::Sched<N, NSQ, NDB, HAS_S, HAS_V>;
-    constexpr int NOPS = SD::NOPS;
-    static_assert(SCH::v.ok, "forward3 schedule");
-    asm volatile("" : "+v"(LrK), "+v"(LtV));
-    const unsigned bK = LrK + lds_addr(Kb + ((j + 1) % NS) * CF::nK);
-    const unsigned tV = LtV + lds_addr(Vb + ((j + NS - 1) % NS) * CF::nV);
-    const int lim = min(qrow, T - 1) - j * BN - 4 * hf;
-    float lt[N];
-    constexpr int RBN = R + 1, RTN = (R + 1) / 2 + 1;
-    i32x4 rb[RBN];
-    lds64 rt[RTN][4];
-    auto issue = [&](auto S_) {
-      constexpr int s = decltype(S_)::value;
-      constexpr fw3::Op o = SCH::v.ops[s];
-      if constexpr (o.kind == fw3::SC) ds128<o.i * BN * ROWB + o.b * 32 * ROWB>(rb[SCH::v.rid[s] % RBN], bK ^ (32 * o.a));
-      else if constexpr (o.c == 0) tr_issue<VROWB, 32 * o.b>(rt[SCH::v.tid[s] % RTN], tV ^ (64 * o.a), tV ^ (64 * o.a + 32));
-    };
-    auto piece = [&](auto P_) {
-      constexpr int pi = decltype(P_)::value, i = pi / SD::PIECES, jj = pi % SD::PIECES;
-      constexpr int kb = jj / 8, r0 = (jj % 8) * 2;
-      if constexpr (jj == 0) lt[i] = 0.f;
-      // the compares stay in their piece (hoisted, the 32 lane masks of a tile fill the SGPRs)
-      int lm = lim;
-      if constexpr (MASK) asm volatile("" : "+v"(lm));
-#pragma unroll
-      for (int r = r0; r < r0 + 2; ++r) {
-        float x = sa[CUR][i][kb][r];
-        if constexpr (MASK) x = (kb * 32 + (r & 3) + 8 * (r >> 2) > lm) ? -INFINITY : x;
-        const float e = exp2_fast(fmaf(x, p.sl2, -m[i]));
-        sa[CUR][i][kb][r] = e;
-        lt[i] += e;
-      }
-      if constexpr (jj == SD::PIECES - 1) {
-        l[i] += lt[i];
-        bad = (lt[i] <= LSMAX) ? bad : 1.f;
-      }
-    };
-    auto pack = [&](auto K_) {
-      constexpr int k = decltype(K_)::value, i = k / 4, x = k % 4;
-      pk[i][x] = O::template pack<x % 2>(sa[CUR][i][x / 2]);
-    };
-    if constexpr (!DTA_FWD3_SPREAD) stage_kv(kt_dma);
-    sfor<(R < NOPS ? R : NOPS)>([&](auto S_) { issue(S_); });
-    sfor<NOPS>([&](auto S_) {
-      constexpr int s = decltype(S_)::value;
-      constexpr fw3::Op o = SCH::v.ops[s];
-      if constexpr (s + R < NOPS) issue(std::integral_constant<int, s + R>{});
-      // this wave's LDS-DMA pieces of tile kt_dma, spread over the stream (issued in one
-      // burst they held the MFMAs for ~60+ cycles each)
-      sfor<KR::MYP>([&](auto U) {
-        constexpr int u = decltype(U)::value;
-        if constexpr (DTA_FWD3_SPREAD && s == (u + 1) * NOPS / (KR::MYP + 1))
-          KR::template issue_one<u>(gk, p.k.st, gv, p.v.st, kt_dma * BN, kt_dma < ntiles ? T : 0,
-                                    Kb + (kt_dma % NS) * CF::nK, Vb + (kt_dma % NS) * CF::nV, wave, doff[u]);
-      });
-      sfor<SCH::v.npack[s]>([&](auto K) { pack(std::integral_constant<int, SCH::v.pkk[s][decltype(K)::value]>{}); });
-      if constexpr (SCH::v.nreads[s] > 0) lgkm_wait<SCH::v.pending(s, R)>();
-      if constexpr (o.kind == fw3::SC) {
-        i32x4& kr = rb[SCH::v.rid[s] % RBN];
-        asm volatile("" : "+v"(kr));
-        f32x16& sx = sa[NXT][o.i][o.b];
-        sx = O::mma(__builtin_bit_cast(frag, kr), qf[o.i][o.a], o.a == 0 ? f32x16{} : sx);
-      } else {
-        lds64 (&tr)[4] = rt[(o.c == 0 ? SCH::v.tid[s] : SCH::v.tid[s - 1]) % RTN];
-        if constexpr (o.c == 0) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) asm volatile("" : "+v"(tr[q]));
-        }
-        mfma_agpr<(o.b == 0 && o.c == 0)>(acc[o.i][o.a], tr_frag<E>(tr, o.c), pk[o.i][o.b * 2 + o.c], hold);
-      }
-      sfor<SCH::v.npiece[s]>([&](auto K) { piece(std::integral_constant<int, SCH::v.pp[s][decltype(K)::value]>{}); });
-      __builtin_amdgcn_sched_barrier(0);
-    });
-    sfor<SCH::v.npack[NOPS]>([&](auto K) { pack(std::integral_constant<int, SCH::v.pkk[NOPS][decltype(K)::value]>{}); });
-    // the O_i^T accumulators are written by asm MFMAs whose latency the compiler does not
-    // see: before any register-allocator copy between AGPRs at the next control-flow
-    // merge, the last MFMA must have landed
-    dq2_acc_fence();
-    acc_pin(acc);
-    mfma_release(hold);
-  };
-
-  for (int pass = 0; pass < 2; ++pass) {
-    if (pass == 1) {
-      // exact row maxima: S^T over every live tile
-#pragma unroll
-      for (int i = 0; i < N; ++i) m[i] = -INFINITY;
-      stage_kv(0); stage_kv(1); stage_kv(2); stage_kv(3);
-      for (int kt = 0; kt < ntiles; ++kt) {
-        if (kt > 0) stage_kv(kt + 3);
-        wait_tiles(kt, kt + 3);
-        lds_barrier();
-        if (kt < nlive) {
-          s_tile(kt, sa[0]);
-          mask_tile(kt, sa[0]);
-#pragma unroll
-          for (int i = 0; i < N; ++i) {
-            float mx = -INFINITY;
-#pragma unroll
-            for (int kb = 0; kb < NKB; ++kb)
-#pragma unroll
-              for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sa[0][i][kb][r]);
-            m[i] = fmaxf(m[i], wave_max_halves(mx) * p.sl2);
-          }
-        }
-        lds_barrier();
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-      l[i] = 0.f;
-#pragma unroll
-      for (int d = 0; d < NDB; ++d) acc[i][d] = f32x16{};
-    }
-    bad = 0.f;
-    // prologue: tiles 0..3 in flight; S^T and P of tile 0 (pass 0: its maxima), S^T of tile 1
-    stage_kv(0); stage_kv(1); stage_kv(2); stage_kv(3);
-    wait_tiles(1, 3);
-    lds_barrier();
-    if (nlive > 0) {
-      s_tile(0, sa[0]);
-      if (nfull == 0) mask_tile(0, sa[0]);
-      if (pass == 0) {
-#pragma unroll
-        for (int i = 0; i < N; ++i) {
-          float mx = -INFINITY;
-#pragma unroll
-          for (int kb = 0; kb < NKB; ++kb)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sa[0][i][kb][r]);
-          m[i] = wave_max_halves(mx) * p.sl2;
-        }
-      }
-      p_tile(sa[0]);
-      if (nlive > 1) s_tile(1, sa[1]);
-    }
-    wait_tiles(2, 3);
-    lds_barrier();
-    // iteration j: products of tile j-1, P of tile j, S^T of tile j+1; one barrier per
-    // iteration for every wave, each wave's iterations in loops of one stream each
-    using T_ = std::true_type;
-    using F_ = std::false_type;
-    using C0 = std::integral_constant<int, 0>;
-    using C1 = std::integral_constant<int, 1>;
-    auto close = [&](int j) {
-      wait_tiles(j + 2, j + 3);
-      lds_barrier();
-    };
-    int j = 1;
-    // tiles 1 .. nlive - 2: unmasked, two per trip (the S^T buffers' roles stay compile-time)
-    for (; j + 1 <= nlive - 2; j += 2) {
-      iter(j, T_{}, T_{}, F_{}, C1{}, j + 3);
-      close(j);
-      iter(j + 1, T_{}, T_{}, F_{}, C0{}, j + 4);
-      close(j + 1);
-    }
-    if (j <= nlive - 2) {
-      iter(j, T_{}, T_{}, F_{}, C1{}, j + 3);
-      close(j);
-      ++j;
-    }
-    // the diagonal tile nlive - 1 (masked; its S^T was issued one iteration earlier)
-    if (j == nlive - 1) {
-      // one instance of this stream: its scores moved into the first buffer (two instances
-      // merging into the last products made the allocator copy O_i^T between AGPRs)
-      if (j & 1) {
-#pragma unroll
-        for (int i = 0; i < N; ++i)
-#pragma unroll
-          for (int kb = 0; kb < NKB; ++kb) sa[0][i][kb] = sa[1][i][kb];
-      }
-      iter(j, F_{}, T_{}, T_{}, C0{}, j + 3);
-      close(j);
-      ++j;
-    }
-    // the last products
-    if (j == nlive) {
-      iter(j, F_{}, F_{}, F_{}, C0{}, j + 3);
-      close(j);
-      ++j;
-    }
-    for (j = max(j, 1); j <= ntiles; ++j) {
-      stage_kv(j + 3);
-      close(j);
-    }
-    if (pass == 1) break;
-    int* flag = reinterpret_cast<int*>(Kb);
-    const bool mine = __any(wave_live && bad != 0.f);
-    if (lane == 0) flag[wave] = mine ? 1 : 0;
-    lds_barrier();
-    bool any = false;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) any |= flag[w] != 0;
-    lds_barrier();
-    if (!any) break;
-  }
-  dq2_acc_fence();
-  acc_pin(acc);
-  mfma_release(hold);
-
-  if (!wave_live || qrow >= T) return;
-  float inv[N];
-#pragma unroll
-  for (int i = 0; i < N; ++i) {
-    const float lt = wave_sum_halves(l[i]);
-    inv[i] = 1.f / lt;
-    if (hf == 0) p.lse[(((int64_t)(br + i) * p.B + b) * p.H + hh) * T + qrow] = -(m[i] + __builtin_log2f(lt));
-  }
-  E* go = reinterpret_cast<E*>(p.o.p) + b * p.o.sb + (int64_t)qrow * p.o.st + hh * p.o.sh;
-  const int64_t gob = b * p.obr.sb + (int64_t)qrow * p.obr.st + hh * p.obr.sh + br * p.obr.si;
-#pragma unroll
-  for (int d = 0; d < NDB; ++d)
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int e = d * 32 + 8 * g + 4 * hf;
-      float o0 = 0.f, o1 = 0.f, o2 = 0.f, o3 = 0.f;
-#pragma unroll
-      for (int i = 0; i < N; ++i) {
-        const float a0 = acc[i][d][4 * g + 0] * inv[i], a1 = acc[i][d][4 * g + 1] * inv[i];
-        const float a2 = acc[i][d][4 * g + 2] * inv[i], a3 = acc[i][d][4 * g + 3] * inv[i];
-        store_ob4(p.obr.p, gob + i * p.obr.si + e, p.ob16, a0, a1, a2, a3);
-        const float c = nsp > 1 ? 1.f : p.coef[hh * p.cst + i];
-        o0 = fmaf(c, a0, o0); o1 = fmaf(c, a1, o1); o2 = fmaf(c, a2, o2); o3 = fmaf(c, a3, o3);
-      }
-      if (nsp == 1) store4<E>(go + e, o0, o1, o2, o3);
-    }
-}
-
-// --------------------------- backward: dK, dV, two query sub-blocks per step ---
-// attn_dkdv2_kernel: attn_dkdv_kernel re-planned like attn_dq2_kernel -- one wave per SIMD,
-// 4 waves x 32 keys = 128 keys per workgroup, 64-row query steps (two 32-row sub-blocks
-// per step from a TileRing<BQ = 64> LDS-DMA ring).  The wave's own K_i rows (prescaled by
-// sl2) and V rows are loop-invariant MFMA operands: loaded once into AGPRs.  dK_i and dV
-// accumulate in AGPRs (mfma_agpr).  Each step is a compile-time MFMA stream -- per unit
-// u = (branch, sub-block) the S' chain seeded with the -LSE rows, per sub-block the dP chain
-// seeded with -delta_0 (and, for branches i >= 1, one more seeded MFMA adding
-// delta_0 - delta_i), the dK_i and dV products -- with each unit's exp / dS / combined-P
-// VALU placed into the slots of MFMAs that do not depend on it (Kv2Sched).
-namespace kv2 {
-enum : int { SS = 0, SC = 1, DS = 2, DC = 3, XS = 4, CK = 5, CV = 6 };
-struct Op { int kind = 0, u = 0, qs = 0, i = 0, a = 0, c = 0; };
-constexpr int PIECES = 8;      // VALU pieces per unit: 16 elements, two at a time
-
-template <int N, int NSQ, int NSV, int NHB, int NVB>
-struct Sched {
-  static constexpr int U = 2 * N, SR = 2;
-  static constexpr int NOPS = U * (1 + NSQ) + 2 * (1 + NSV) + 2 * (N - 1) + U * NHB * 2 + 2 * NVB * 2;
-  static constexpr int ui(int u) { return N - 1 - u / 2; }
-  static constexpr int uq(int u) { return u % 2; }
-  static constexpr bool first_of_qs(int u) { return u < 2; }        // branch N-1: pc starts here
-  static constexpr bool last_of_qs(int u) { return u >= U - 2; }    // branch 0: pc complete
-  Op ops[NOPS];
-  int s0[U] = {}, s1[U] = {}, c0[U] = {}, d1[2] = {}, x1[U] = {}, v0[2] = {};
-  int E[U] = {}, Dl[U] = {};
-  int npiece[NOPS] = {};
-  int pu[NOPS][PIECES * 4] = {};
-  int nreads[NOPS] = {};
-  int rid[NOPS] = {};          // b128 reads (Q / dO fragments)
-  int tid[NOPS] = {};          // tr blocks (dK: Q^T, dV: dO^T)
-  bool ok = true;
-  constexpr Op mk(int kind, int u, int qs, int i, int a, int c) const {
-    Op o; o.kind = kind; o.u = u; o.qs = qs; o.i = i; o.a = a; o.c = c; return o;
-  }
-  constexpr void add_s(int& n, int u) {
-    s0[u] = n;
-    ops[n++] = mk(SS, u, uq(u), ui(u), 0, 0);
-    for (int st = 0; st < NSQ; ++st) ops[n++] = mk(SC, u, uq(u), ui(u), st, 0);
-    s1[u] = n - 1;
-  }
-  constexpr void add_d(int& n, int qs) {
-    ops[n++] = mk(DS, 0, qs, 0, 0, 0);
-    for (int s = 0; s < NSV; ++s) ops[n++] = mk(DC, 0, qs, 0, s, 0);
-    d1[qs] = n - 1;
-    for (int u = 0; u < U; ++u)
-      if (uq(u) == qs && ui(u) >= 1) { ops[n] = mk(XS, u, qs, ui(u), 0, 0); x1[u] = n++; }
-  }
-  constexpr void add_ck(int& n, int u) {
-    c0[u] = n;
-    for (int d = 0; d < NHB; ++d)
-      for (int ks = 0; ks < 2; ++ks) ops[n++] = mk(CK, u, uq(u), ui(u), d, ks);
-  }
-  constexpr void add_cv(int& n, int qs) {
-    v0[qs] = n;
-    for (int d = 0; d < NVB; ++d)
-      for (int ks = 0; ks < 2; ++ks) ops[n++] = mk(CV, 0, qs, 0, d, ks);
-  }
-  constexpr Sched() {
-    int n = 0;
-    add_s(n, 0); add_d(n, 0);
-    add_s(n, 1); add_d(n, 1);
-    for (int u = 2; u < U; ++u) { add_s(n, u); add_ck(n, u - 2); }
-    add_ck(n, U - 2); add_cv(n, 0);
-    add_ck(n, U - 1); add_cv(n, 1);
-    if (n != NOPS) ok = false;
-    for (int u = 0; u < U; ++u) {
-      int e = s1[u] > d1[uq(u)] ? s1[u] : d1[uq(u)];
-      if (ui(u) >= 1 && x1[u] > e) e = x1[u];
-      E[u] = e + 1;
-      Dl[u] = c0[u] - 1;
-      if (last_of_qs(u) && v0[uq(u)] - 1 < Dl[u]) Dl[u] = v0[uq(u)] - 1;
-      if (u + SR < U && s0[u + SR] < Dl[u]) Dl[u] = s0[u + SR];
-      // the next unit of the same sub-block accumulates into the same combined P: keep order
-    }
-    int load[NOPS] = {};
-    int prev_end[2] = {0, 0};
-    for (int u = 0; u < U; ++u) {
-      const int lo = E[u] > prev_end[uq(u)] ? E[u] : prev_end[uq(u)];
-      int cap = 1;
-      for (;; ++cap) {
-        int room = 0;
-        for (int x = lo; x < Dl[u]; ++x) room += load[x] < cap ? cap - load[x] : 0;
-        if (room >= PIECES || cap >= PIECES * 4) break;
-      }
-      int j = 0, last = lo;
-      for (int x = lo; x < Dl[u] && j < PIECES; ++x)
-        while (load[x] < cap && j < PIECES) {
-          if (npiece[x] < PIECES * 4) pu[x][npiece[x]++] = u * PIECES + j; else ok = false;
-          ++load[x];
-          ++j;
-          last = x;
-        }
-      if (j < PIECES) ok = false;
-      prev_end[uq(u)] = last;
-    }
-    int nb = 0, ntr = 0;
-    for (int s = 0; s < NOPS; ++s) {
-      const Op& o = ops[s];
-      if (o.kind == SC || o.kind == DC) { rid[s] = nb++; nreads[s] = 1; }
-      else if ((o.kind == CK || o.kind == CV) && o.c == 0) { tid[s] = ntr++; nreads[s] = 4; }
-    }
-  }
-  constexpr int pending(int s, int R) const {
-    int c = 0;
-    for (int x = s + 1; x <= s + R && x < NOPS; ++x) c += nreads[x];
-    return c;
-  }
-};
-template <int N, int NSQ, int NSV, int NHB, int NVB>
-struct Hold { static constexpr Sched<N, NSQ, NSV, NHB, NVB> v{}; };
-}  // namespace kv2
-
-#ifndef DTA_DKDV2
-#define DTA_DKDV2 1
-#endif
-template <class E, int HS, int N, int DV>
-struct Kv2Cfg {
-  static constexpr int NW = 4, BK = 128, BQ = 64;
-  using RG = TileRing<E, HS, N, DV, NW, true, BQ, true>;
-  static constexpr int NS = (160 * 1024) / RG::SB >= 4 ? 4 : ((160 * 1024) / RG::SB >= 3 ? 3 : 2);
-  static constexpr int bytes = NS * RG::SB;
-  static constexpr int NHB = HS / 32, NVB = DV / 32;
-  // VGPRs: dP (2 sub-blocks) + the branch-corrected dP of branches >= 1, two S' sets, packed
-  // dS of every unit, combined P and its packs, seeds, read buffers; AGPRs: dK, dV, K, V
-  static constexpr int vregs = 2 * 16 + 2 * (N - 1) * 16 + 2 * 16 + 2 * N * 8 + 2 * 16 + 2 * 8 + 4 * N * 4 + 80;
-  static constexpr int aregs = N * NHB * 16 + NVB * 16 + N * HS / 4 + DV / 4 + 4;
-  static constexpr bool shape_ok = DTA_DKDV2 && std::is_same<E, __bf16>::value && (HS == 32 || HS == 64 || HS == 128) &&
-                                   (DV == HS || DV == 2 * HS) && DV <= 128 && RG::ok && 2 * RG::SB <= 160 * 1024 &&
-                                   vregs <= 256 && aregs <= 256;
-  template <bool S, int = 0> struct Sok { static constexpr bool v = false; };
-  template <int X> struct Sok<true, X> { static constexpr bool v = kv2::Hold<N, HS / 16, DV / 16, HS / 32, DV / 32>::v.ok; };
-  static constexpr bool ok = Sok<shape_ok>::v;
-};
-
-template <class E, int HS, int N, int DV>
-__global__ __launch_bounds__(256, 1)
-void attn_dkdv2_kernel(BwdParams p) {
-  using O = Ops<E>;
-  using frag = typename O::frag;
-  using CF = Kv2Cfg<E, HS, N, DV>;
-  using RG = typename CF::RG;
-  constexpr int NW = CF::NW, BK = CF::BK, BQ = CF::BQ, KS = O::KSTEP, NS = CF::NS;
-  constexpr int NSQ = HS / KS, NSV = DV / KS, NHB = HS / 32, NVB = DV / 32;
-  constexpr int QROWB = RG::HSP * (int)sizeof(E), DROWB = RG::DVP * (int)sizeof(E);
-  constexpr int R = DTA_DQ2_R;
-  using SCH = kv2::Hold<N, NSQ, NSV, NHB, NVB>;
-  using SD = kv2::Sched<N, NSQ, NSV, NHB, NVB>;
-  constexpr int NOPS = SD::NOPS, U = 2 * N;
-  static_assert(SCH::v.ok, "dK/dV2 schedule");
-
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* ringb = smem;                     // NS stages of TileRing<BQ = 64>
-
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  int tid = threadIdx.x, lane = tid & 63;
-  int hf = lane >> 5, c32 = lane & 31;
-  int bx, by, bz, lin;
-  lpt_order(bx, by, bz, lin);
-  const int kblk = bx;
-  const int hh = by, b = bz;
-  const int T = p.T;
-  const int kb0 = kblk * BK, kw0 = kb0 + wave * 32;
-  const int krow = kw0 + c32;
-  const E* gq = reinterpret_cast<const E*>(p.q.p) + b * p.q.sb + hh * p.q.sh;
-  const E* gk = reinterpret_cast<const E*>(p.k.p) + b * p.k.sb + hh * p.k.sh;
-  const E* gv = reinterpret_cast<const E*>(p.v.p) + b * p.v.sb + hh * p.v.sh;
-  const E* gdo = reinterpret_cast<const E*>(p.dout.p) + b * p.dout.sb + hh * p.dout.sh;
-  const int64_t rowvec = ((int64_t)b * p.H + hh) * T;
-  const int64_t bstride = (int64_t)p.B * p.H * T;
-
-  float coef[N];
-#pragma unroll
-  for (int i = 0; i < N; ++i) coef[i] = p.coef[hh * p.cst + i];
-  // this wave's K_i rows (x sl2) and V rows: B operands of S' and dP, in AGPRs
-  frag kf[N][NSQ], vf[NSV];
-#pragma unroll
-  for (int i = 0; i < N; ++i)
-#pragma unroll
-    for (int st = 0; st < NSQ; ++st) {
-      frag f = krow < T ? O::load_global(gk + (int64_t)krow * p.k.st + i * p.k.si + st * KS + hf * O::KH) : O::zero();
-#pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] = (E)((float)f[j] * p.sl2);
-      kf[i][st] = f;
-    }
-#pragma unroll
-  for (int s = 0; s < NSV; ++s)
-    vf[s] = krow < T ? O::load_global(gv + (int64_t)krow * p.v.st + s * KS + hf * O::KH) : O::zero();
-  frag f_one = O::zero();
-  if (hf == 0) { f_one[0] = (E)1.f; f_one[1] = (E)1.f; }
-#pragma unroll
-  for (int i = 0; i < N; ++i)
-#pragma unroll
-    for (int st = 0; st < NSQ; ++st) asm volatile("" : "+a"(kf[i][st]));
-#pragma unroll
-  for (int s = 0; s < NSV; ++s) asm volatile("" : "+a"(vf[s]));
-
-  uint32_t roff[RG::MYP];
-  RG::offsets(p, bstride, wave, lane, roff);
-  const int nsteps = kb0 < T ? (T - kb0 + BQ - 1) / BQ : 0;
-  auto stage_q = [&](int q0, int buf) {
-    RG::issue_pre(p, gq, gdo, p.lse + rowvec, p.delta + rowvec, bstride, q0, T, ringb + buf * RG::SB, wave, roff);
-  };
-  const int tile_pieces = RG::pieces(wave);
-  for (int j = 0; j < NS - 1; ++j)
-    if (j < nsteps) stage_q(kb0 + j * BQ, j);
-  wait_vm(tile_pieces * max(0, min(NS - 1, nsteps) - 1));
-  lds_barrier();
-
-  f32x16 dk[N][NHB], dv[NVB];
-  MfmaHold hold{};
-#pragma unroll
-  for (int i = 0; i < N; ++i)
-#pragma unroll
-    for (int d = 0; d < NHB; ++d) dk[i][d] = f32x16{};
-#pragma unroll
-  for (int d = 0; d < NVB; ++d) dv[d] = f32x16{};
-
-  int LrQ = row_lane<QROWB>(lane), LrD = row_lane<DROWB>(lane), LtQ = tr_lane<QROWB>(lane), LtD = tr_lane<DROWB>(lane);
-
-  auto body = [&](int t, auto MASKED) {
-    constexpr bool MASK = decltype(MASKED)::value;
-    asm volatile("" : "+v"(LrQ), "+v"(LrD), "+v"(LtQ), "+v"(LtD));
-    frag one = f_one;
-    asm volatile("" : "+v"(one));
-    const int buf = t % NS, qs0 = kb0 + t * BQ;
-    const char* sg = ringb + buf * RG::SB;
-    const unsigned sb = lds_addr(sg);
-    const unsigned bQ = LrQ + sb, bD = LrD + sb, tQ = LtQ + sb, tD = LtD + sb;
-    const float* Lc = reinterpret_cast<const float*>(sg + RG::OFF_L);
-    const float* Gc = reinterpret_cast<const float*>(sg + RG::OFF_G);
-    // row seeds (row = query = lane & 31 of an A operand): -LSE_i, -delta_0, delta_0 - delta_i
-    frag sseed[N][2], dseed[2], xseed[N > 1 ? N : 2][2];
-#pragma unroll
-    for (int qs = 0; qs < 2; ++qs) {
-      const int r = 32 * qs + (lane & 31);
-#pragma unroll
-      for (int i = 0; i < N; ++i) sseed[i][qs] = seed_frag<E>(Lc[i * BQ + r], lane >> 5);
-      dseed[qs] = seed_frag<E>(Gc[r], lane >> 5);
-#pragma unroll
-      for (int i = 1; i < N; ++i) xseed[i][qs] = seed_frag<E>(Gc[i * BQ + r], lane >> 5);
-    }
-    int lim_lo[2], lim_hi[2];
-#pragma unroll
-    for (int qs = 0; qs < 2; ++qs) {
-      lim_lo[qs] = krow - (qs0 + 32 * qs) - 4 * (lane >> 5);
-      lim_hi[qs] = T - 1 - (qs0 + 32 * qs) - 4 * (lane >> 5);
-    }
-    f32x16 dpa[2], dpx[U > 2 ? U : 1], sa[2], pc[2];
-    frag dsp[U][2], pcp[2][2];
-    constexpr int RBN = R + 1, RTN = (R + 1) / 2 + 1;
-    i32x4 rb[RBN];
-    lds64 rt[RTN][4];
-    auto issue = [&](auto S_) {
-      constexpr int s = decltype(S_)::value;
-      constexpr kv2::Op o = SCH::v.ops[s];
-      if constexpr (o.kind == kv2::SC) {
-        ds128<o.i * RG::QB + o.qs * 32 * QROWB>(rb[SCH::v.rid[s] % RBN], bQ ^ (32 * o.a));
-      } else if constexpr (o.kind == kv2::DC) {
-        ds128<RG::OFF_D + o.qs * 32 * DROWB>(rb[SCH::v.rid[s] % RBN], bD ^ (32 * o.a));
-      } else if constexpr (o.kind == kv2::CK && o.c == 0) {
-        tr_issue<QROWB, 32 * o.qs, o.i * RG::QB>(rt[SCH::v.tid[s] % RTN], tQ ^ (64 * o.a), tQ ^ (64 * o.a + 32));
-      } else if constexpr (o.kind == kv2::CV && o.c == 0) {
-        tr_issue<DROWB, 32 * o.qs, RG::OFF_D>(rt[SCH::v.tid[s] % RTN], tD ^ (64 * o.a), tD ^ (64 * o.a + 32));
-      }
-    };
-    auto piece = [&](auto PU) {
-      constexpr int u = decltype(PU)::value / kv2::PIECES, j = decltype(PU)::value % kv2::PIECES;
-      constexpr int i = SD::ui(u), qs = SD::uq(u), su = u % 2;
-#pragma unroll
-      for (int r = 2 * j; r < 2 * j + 2; ++r) {
-        float arg = sa[su][r];
-        if constexpr (MASK) {
-          const int rc = (r & 3) + 8 * (r >> 2);
-          arg = (rc < lim_lo[qs] || rc > lim_hi[qs]) ? -INFINITY : arg;
-        }
-        const float pr = exp2_fast(arg);
-        if constexpr (SD::first_of_qs(u)) pc[qs][r] = coef[i] * pr;
-        else pc[qs][r] = fmaf(coef[i], pr, pc[qs][r]);
-        sa[su][r] = pr * (i == 0 ? dpa[qs][r] : dpx[U > 2 ? u : 0][r]);
-      }
-      if constexpr (j % 4 == 3) {
-        dsp[u][j / 4] = O::template pack<j / 4>(sa[su]);
-        if constexpr (SD::last_of_qs(u)) pcp[qs][j / 4] = O::template pack<j / 4>(pc[qs]);
-      }
-    };
-    sfor<(R < NOPS ? R : NOPS)>([&](auto S_) { issue(S_); });
-    sfor<NOPS>([&](auto S_) {
-      constexpr int s = decltype(S_)::value;
-      constexpr kv2::Op o = SCH::v.ops[s];
-      if constexpr (s + R < NOPS) issue(std::integral_constant<int, s + R>{});
-      if constexpr (SCH::v.nreads[s] > 0) lgkm_wait<SCH::v.pending(s, R)>();
-      if constexpr (o.kind == kv2::SS) {
-        sa[o.u % 2] = O::mma(sseed[o.i][o.qs], one, f32x16{});
-      } else if constexpr (o.kind == kv2::SC) {
-        i32x4& qr = rb[SCH::v.rid[s] % RBN];
-        asm volatile("" : "+v"(qr));
-        sa[o.u % 2] = O::mma(__builtin_bit_cast(frag, qr), kf[o.i][o.a], sa[o.u % 2]);
-      } else if constexpr (o.kind == kv2::DS) {
-        dpa[o.qs] = O::mma(dseed[o.qs], one, f32x16{});
-      } else if constexpr (o.kind == kv2::DC) {
-        i32x4& dr = rb[SCH::v.rid[s] % RBN];
-        asm volatile("" : "+v"(dr));
-        dpa[o.qs] = O::mma(__builtin_bit_cast(frag, dr), vf[o.a], dpa[o.qs]);
-      } else if constexpr (o.kind == kv2::XS) {
-        dpx[U > 2 ? o.u : 0] = O::mma(xseed[o.i][o.qs], one, dpa[o.qs]);
-      } else {
-        lds64 (&tr)[4] = rt[(o.c == 0 ? SCH::v.tid[s] : SCH::v.tid[s - 1]) % RTN];
-        if constexpr (o.c == 0) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(tr[j]));
-        }
-        if constexpr (o.kind == kv2::CK)
-          mfma_agpr<(s == SCH::v.c0[o.u])>(dk[o.i][o.a], tr_frag<E>(tr, o.c), dsp[o.u][o.c], hold);
-        else
-          mfma_agpr<(s == SCH::v.v0[o.qs])>(dv[o.a], tr_frag<E>(tr, o.c), pcp[o.qs][o.c], hold);
-      }
-      sfor<SCH::v.npiece[s]>([&](auto K) { piece(std::integral_constant<int, SCH::v.pu[s][decltype(K)::value]>{}); });
-      __builtin_amdgcn_sched_barrier(0);
-    });
-  };
-  auto step = [&](int t, auto MASKED, bool live) {
-    if (t + NS - 1 < nsteps) stage_q(kb0 + (t + NS - 1) * BQ, (t + NS - 1) % NS);
-    if (live) body(t, MASKED);
-    wait_vm(tile_pieces * max(0, min(NS - 2, nsteps - 2 - t)));
-    lds_barrier();
-  };
-  // per wave: steps wholly before its first key (nothing to add), its diagonal steps,
-  // the unmasked middle, a ragged tail step
-  const bool wave_keys = kw0 < T;
-  const int tlive = wave_keys ? min(nsteps, (kw0 - kb0) / BQ) : nsteps;
-  const int tfull = wave_keys ? min(nsteps, (kw0 - kb0 + 31 + BQ - 1) / BQ) : nsteps;
-  const int ttail = wave_keys ? max(tfull, nsteps - ((T - kb0) % BQ != 0 ? 1 : 0)) : nsteps;
-  for (int t = 0; t < tlive; ++t) step(t, std::false_type{}, false);
-  for (int t = tlive; t < tfull; ++t) step(t, std::true_type{}, true);
-  for (int t = tfull; t < ttail; ++t) step(t, std::false_type{}, true);
-  for (int t = ttail; t < nsteps; ++t) step(t, std::true_type{}, true);
-  dq2_acc_fence();
-  acc_pin(dk);
-  acc_pin(dv);
-  mfma_release(hold);
-
-  if (!wave_keys || krow >= T) return;
-  E* gdk = reinterpret_cast<E*>(p.dk.p) + b * p.dk.sb + (int64_t)krow * p.dk.st + hh * p.dk.sh;
-#pragma unroll
-  for (int i = 0; i < N; ++i) {
-    const float sc = p.scale * coef[i];
-#pragma unroll
-    for (int d = 0; d < NHB; ++d)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int e = d * 32 + 8 * g + 4 * hf;
-        float a0 = dk[i][d][4 * g] * sc, a1 = dk[i][d][4 * g + 1] * sc;
-        float a2 = dk[i][d][4 * g + 2] * sc, a3 = dk[i][d][4 * g + 3] * sc;
-        if (p.rope) rope_inv4(p.rope, krow, HS, e, a0, a1, a2, a3);
-        store4<E>(gdk + i * p.dk.si + e, a0, a1, a2, a3);
-      }
-  }
-  E* gdv = reinterpret_cast<E*>(p.dv.p) + b * p.dv.sb + (int64_t)krow * p.dv.st + hh * p.dv.sh;
-#pragma unroll
-  for (int d = 0; d < NVB; ++d)
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int e = d * 32 + 8 * g + 4 * hf;
-      float a0 = dv[d][4 * g], a1 = dv[d][4 * g + 1], a2 = dv[d][4 * g + 2], a3 = dv[d][4 * g + 3];
-      if (p.dv_acc) {
-        a0 += (float)gdv[e]; a1 += (float)gdv[e + 1]; a2 += (float)gdv[e + 2]; a3 += (float)gdv[e + 3];
-      }
-      store4<E>(gdv + e, a0, a1, a2, a3);
-    }
-}
-
 // ------------------------------------------------------------ launchers ---
 template <class K>
 static inline int set_smem(K kernel, int bytes) {
@@ -3378,19 +2134,11 @@ __global__ __launch_bounds__(256) void branch_combine_kernel(FwdParams p, Combin
 // softmax: head size 128 at N = 2, cfg5; N = 4 at head size 64, cfg3) or runs one wave
 // per SIMD (N = 3 at head size 64, cfg3).  One-process A/B (profiles/r03_bsplit_ab.json):
 // cfg5 fwd 20.54 -> 12.66 ms, cfg3 N=4 0.744 -> 0.485, N=3 0.409 -> 0.361; cfg2's
-// paired N = 2 plan stays (split: 0.999 -> 1.126).  The macro DTA_FWD_BSPLIT = 0 builds
-// no split at all; the env var DTA_FWD_BSPLIT = 1 also splits the non-auto plans.
+// paired N = 2 plan stays (split: 0.999 -> 1.126).  A/B builds: the macro DTA_FWD_BSPLIT = 0
+// builds no split at all, 1 also splits the non-auto plans (the product build is -1).
 #ifndef DTA_FWD_BSPLIT
 #define DTA_FWD_BSPLIT -1
 #endif
-static inline int fwd_bsplit_env() {
-  static const int v = [] {
-    const char* s = getenv("DTA_FWD_BSPLIT");
-    return s && *s ? atoi(s) : DTA_FWD_BSPLIT;
-  }();
-  return v;
-}
-
 template <class E, int HS, int N, int DV_ = 2 * HS>
 struct Plan {
   static constexpr int DV = DV_;
@@ -3402,8 +2150,6 @@ struct Plan {
                              DkdvCfg<E, HS, N, DV, KVW, KPR, DkdvWaves<E, HS, N, DV>::gr>::bytes <= 160 * 1024;
 };
 
-int launch_attn_fwd3_bf16(const FwdParams& p, hipStream_t st); // attn_bf16_dq2.hip
-static inline bool fwd3_env();
 template <class E, int HS, int N, int DV_, bool DROP>
 int launch_fwd_t(const FwdParams& p, hipStream_t st) {
   using PL = Plan<E, HS, N, DV_>;
@@ -3413,13 +2159,13 @@ int launch_fwd_t(const FwdParams& p, hipStream_t st) {
   constexpr int bytes = FwdCfg<E, HS, N, DVC, NW, FP::QREG, QH>::bytes;
   // auto: the N-branch plan splits dv, or (16-bit, head size >= 64) it is not the paired
   // two-workgroups-per-CU plan (N >= 3, head size 96 / 128: one wave per SIMD).  Auto
-  // plans always split (their N-branch kernel is not built); DTA_FWD_BSPLIT = 1 also
-  // splits the others.
+  // plans always split (their N-branch kernel is not built); an A/B build with
+  // DTA_FWD_BSPLIT = 1 also splits the others.
   constexpr bool CAN = N >= 2 && Plan<E, HS, 1, PL::DV>::ok;
   constexpr bool AUTO = CAN && DTA_FWD_BSPLIT != 0 &&
                         (DVC < PL::DV || (sizeof(E) == 2 && HS >= 64 && !FwdPick<E, HS, N, PL::DV>::pair));
   if constexpr (CAN) {
-    if (AUTO || fwd_bsplit_env() > 0) {
+    if (AUTO || DTA_FWD_BSPLIT > 0) {
       FwdParams q = p;
       q.bsplit = N;
       if (int e = launch_fwd_t<E, HS, 1, DV_, DROP>(q, st)) return e;
@@ -3433,14 +2179,6 @@ int launch_fwd_t(const FwdParams& p, hipStream_t st) {
   if constexpr (AUTO) {
     return -2;       // unreachable
   } else {
-  if constexpr (Fw3Cfg<E, HS, N, PL::DV>::ok && !DROP) {
-    // one wave per SIMD, key tiles software-pipelined (attn_fwd3_kernel, unit attn_bf16_dq2.hip)
-    if (!p.rope && kv_layout_ok(p, (int)sizeof(E)) && fwd3_env()) {
-      FwdParams q = p;
-      q.N = N;            // a branch-split launch runs the N = 1 instance with p.N = the call's N
-      return launch_attn_fwd3_bf16(q, st);
-    }
-  }
   const int nsp = (N == 1 && p.bsplit > 1) ? p.bsplit : 1;
   dim3 grid((p.T + NW * 32 - 1) / (NW * 32), p.H * nsp * (PL::DV / DVC), p.B);
   auto run = [&](auto SRDV) -> int {
@@ -3459,58 +2197,6 @@ int launch_fwd_t(const FwdParams& p, hipStream_t st) {
   }
 }
 
-int launch_attn_dq2_bf16(const BwdParams& p, hipStream_t st);   // attn_bf16_dq2.hip
-int launch_attn_dkdv2_bf16(const BwdParams& p, hipStream_t st); // attn_bf16_dq2.hip
-template <class E, int HS, int N, int DV>
-int launch_dkdv2_t(const BwdParams& p, hipStream_t st) {
-  using C2 = Kv2Cfg<E, HS, N, DV>;
-  auto kern = attn_dkdv2_kernel<E, HS, N, DV>;
-  if (int e = set_smem(kern, C2::bytes)) return e;
-  hipLaunchKernelGGL(kern, dim3((p.T + C2::BK - 1) / C2::BK, p.H, p.B), dim3(256), C2::bytes, st, p);
-  return (int)hipGetLastError();
-}
-template <class E, int HS, int N, int DV>
-int launch_fwd3_t(const FwdParams& p, hipStream_t st) {
-  using C3 = Fw3Cfg<E, HS, N, DV>;
-  auto kern = attn_fwd3_kernel<E, HS, N, DV>;
-  if (int e = set_smem(kern, C3::bytes)) return e;
-  const int nsp = (N == 1 && p.bsplit > 1) ? p.bsplit : 1;
-  hipLaunchKernelGGL(kern, dim3((p.T + C3::BM - 1) / C3::BM, p.H * nsp, p.B), dim3(256), C3::bytes, st, p);
-  return (int)hipGetLastError();
-}
-// DTA_FWD3 = 1 in the environment selects attn_fwd3_kernel where it is built
-static inline bool fwd3_env() {
-  static const bool v = [] {
-    const char* s = getenv("DTA_FWD3");
-    return s && *s == '1';           // opt-in until verified on the GPU
-  }();
-  return v;
-}
-// DTA_DKDV2 = 0 in the environment keeps attn_dkdv_kernel where attn_dkdv2_kernel is built
-static inline bool dkdv2_env() {
-  static const bool v = [] {
-    const char* s = getenv("DTA_DKDV2");
-    return s && *s == '1';           // opt-in until verified on the GPU
-  }();
-  return v;
-}
-template <class E, int HS, int N, int DV>
-int launch_dq2_t(const BwdParams& p, hipStream_t st) {
-  using C2 = Dq2Cfg<E, HS, N, DV>;
-  auto kern = attn_dq2_kernel<E, HS, N, DV>;
-  if (int e = set_smem(kern, C2::bytes)) return e;
-  hipLaunchKernelGGL(kern, dim3((p.T + C2::BM - 1) / C2::BM, p.H, p.B), dim3(256), C2::bytes, st, p);
-  return (int)hipGetLastError();
-}
-// DTA_DQ2 = 0 in the environment keeps attn_dq_kernel where attn_dq2_kernel is built (A/B)
-static inline bool dq2_env() {
-  static const bool v = [] {
-    const char* s = getenv("DTA_DQ2");
-    return s && *s == '1';           // opt-in until verified on the GPU
-  }();
-  return v;
-}
-
 template <class E, int HS, int N, int DV_, bool DROP>
 int launch_dq_t(const BwdParams& p, hipStream_t st) {
   using PL = Plan<E, HS, N, DV_>;
@@ -3521,11 +2207,6 @@ int launch_dq_t(const BwdParams& p, hipStream_t st) {
   constexpr bool B32 = DP::B32;
   using CF = DqCfg<E, HS, N, DV, NW, QR, QH, B32>;
   constexpr int bytes = CF::bytes;
-  if constexpr (Dq2Cfg<E, HS, N, DV>::ok && !DROP && KvRing<E, HS, N, DV, 64, 4>::ok) {
-    // one wave per SIMD, two 32-row blocks per wave (attn_dq2_kernel, its own unit:
-    // attn_bf16_dq2.hip)
-    if (kv_layout_ok(p, (int)sizeof(E)) && dq2_env()) return launch_attn_dq2_bf16(p, st);
-  }
   dim3 grid((p.T + NW * 32 - 1) / (NW * 32), p.H, p.B);
   auto run = [&](auto F32, auto SRDV) -> int {
     auto kern = attn_dq_kernel<E, HS, N, DV, NW, QR, decltype(F32)::value, decltype(SRDV)::value, DROP, QH, B32>;
@@ -3552,10 +2233,6 @@ int launch_dkdv_t(const BwdParams& p, hipStream_t st) {
   constexpr bool PR = KW::pair && !GR;
   using CF = DkdvCfg<E, HS, N, DV, NW, PR, GR>;
   constexpr int bytes = CF::bytes;
-  if constexpr (Kv2Cfg<E, HS, N, DV>::ok && !DROP) {
-    // one wave per SIMD, 64-row query steps (attn_dkdv2_kernel, its own unit: attn_bf16_dq2.hip)
-    if (ring_layout_ok(p, (int)sizeof(E)) && dkdv2_env()) return launch_attn_dkdv2_bf16(p, st);
-  }
   dim3 grid((p.T + NW * 32 - 1) / (NW * 32), p.H, p.B);
   dim3 block(NW * 64);
   // one-wave-per-SIMD 16-bit plans (4 waves, not paired) have 512 registers: dK and dV
