@@ -306,14 +306,16 @@ int dta_attn_bwd(const dta_attn_bwd_args* a, void* stream) {
     return q;
   };
   int e = 0;
-  // the dK/dV grouping must see delta rows encoded for its own groups (see
-  // bwd_group_cap): with dropout the rows hold delta_i itself; beyond 64 branches, or
-  // where the re-base does not apply, both stages take the dK/dV grouping
-  const int kcap = bwd_group_cap(a->dtype, p.HS, p.N, true);
-  int qcap = bwd_group_cap(a->dtype, p.HS, p.N, false);
-  if (p.drop_thr || p.N > 64) qcap = kcap;
-  const uint64_t qstarts = qcap == kcap ? 0 : group_starts(a->dtype, p.HS, p.N, p.DV, qcap);
-  const uint64_t kstarts = qcap == kcap ? 0 : group_starts(a->dtype, p.HS, p.N, p.DV, kcap);
+  // the dK/dV grouping must see delta rows encoded for its own groups (see bwd_group_cap)
+  if (a->group_max_dq < 0 || a->group_max_dkdv < 0) return DTA_ERR_INVALID;
+  const int kcap = a->group_max_dkdv ? a->group_max_dkdv : bwd_group_cap(a->dtype, p.HS, p.N, true);
+  int qcap = a->group_max_dq ? a->group_max_dq : bwd_group_cap(a->dtype, p.HS, p.N, false);
+  // beyond 64 branches the group-start masks do not fit: both stages take the dK/dV grouping
+  if (p.N > 64) qcap = kcap;
+  // with dropout the delta rows hold delta_i itself (no group encoding): nothing to re-base
+  const bool rebase = qcap != kcap && !p.drop_thr;
+  const uint64_t qstarts = rebase ? group_starts(a->dtype, p.HS, p.N, p.DV, qcap) : 0;
+  const uint64_t kstarts = rebase ? group_starts(a->dtype, p.HS, p.N, p.DV, kcap) : 0;
   if (stages & DTA_BWD_DQ) {
     for (int g0 = 0, ng; g0 < p.N; g0 += ng) {
       ng = branch_group(a->dtype, p.HS, p.N - g0, p.DV, qcap);
@@ -386,7 +388,9 @@ int dta_rope(const dta_rope_args* a, void* stream) {
   if (a->head_size % 8) return DTA_ERR_UNSUPPORTED;
   if ((int64_t)a->B * a->T == 0) return DTA_OK;
   const int src_dtype = a->src_f32 ? DTA_F32 : a->dtype;
-  if (!ok_tensor(a->src, src_dtype, true) || !ok_tensor(a->dst, a->dtype, true) || !a->freqs) return DTA_ERR_INVALID;
+  // the kernel reads the freqs table by 16-byte vectors (as the attention entry points require)
+  if (!ok_tensor(a->src, src_dtype, true) || !ok_tensor(a->dst, a->dtype, true) || !aligned_ptr(a->freqs))
+    return DTA_ERR_INVALID;
   RopeParams p{};
   p.src = t5(a->src); p.dst = t5(a->dst); p.freqs = a->freqs;
   p.B = a->B; p.T = a->T; p.H = a->H; p.N = a->n_terms; p.HS = a->head_size; p.inverse = a->inverse ? 1 : 0;

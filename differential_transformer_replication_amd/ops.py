@@ -121,6 +121,24 @@ def _obr_dtype(dtype: torch.dtype) -> torch.dtype:
     return torch.float32
 
 
+# Backward branch-group caps handed to dta_attn_bwd (ABI 7 group_max_dq / group_max_dkdv);
+# (0, 0) = the library's per-stage defaults.  Tests set them with ``bwd_group_caps`` to run
+# every built native N-branch backward plan.
+_BWD_GROUP_MAX = [0, 0]
+
+
+@contextlib.contextmanager
+def bwd_group_caps(dq: int, dkdv: int):
+    """Within the block, backward passes run dQ in branch groups of at most ``dq`` and
+    dK/dV in groups of at most ``dkdv`` (0 = the library default for that stage)."""
+    old = list(_BWD_GROUP_MAX)
+    _BWD_GROUP_MAX[:] = [int(dq), int(dkdv)]
+    try:
+        yield
+    finally:
+        _BWD_GROUP_MAX[:] = old
+
+
 class _DiffAttention(torch.autograd.Function):
     @staticmethod
     def forward(ctx, qkv: Tensor, coef: Tensor, H: int, N: int, hs: int, freqs: Optional[Tensor], dv: int,
@@ -196,7 +214,7 @@ class _DiffAttention(torch.autograd.Function):
                              _lib.tensor5(dq), _lib.tensor5(dk), _lib.tensor5(dvv),
                              dcoef.data_ptr(), delta.data_ptr(), None, _lib.BWD_PRE,
                              freqs.data_ptr() if freqs is not None else None, dcp.data_ptr(), ctx.drop[1],
-                             _lib.dtype_code(obr.dtype))
+                             _lib.dtype_code(obr.dtype), *_BWD_GROUP_MAX)
         _lib.check(lib.dta_attn_bwd(a, stream))
         a.stages = _lib.BWD_DQ
         with TIMER.region("attn_bwd_dq"):

@@ -26,8 +26,9 @@
  *   Q, K   [b][t][h][i][d]   i < n_terms (the N softmax branches), d < head_size
  *   V, O   [b][t][h][e]      e < dv (dv = 2*head_size for diff attention; dv = head_size with n_terms = 1
  *                             for standard attention, head_size 64 or 128)
- *   Obr    [i][b][t][h][e]   fp32 per-branch normalised outputs A_i V (saved for bwd:
- *                             delta_i = <dO, O_i> and d(coef) come from them)
+ *   Obr    [i][b][t][h][e]   per-branch normalised outputs A_i V, fp32 (default) or fp16
+ *                             (obr_dtype, 16-bit activations only); saved for bwd:
+ *                             delta_i = <dO, O_i> and d(coef) come from them
  *   LSE    [i][b][h][t]      fp32, NEGATED log2-sum-exp of the scaled scores (-log2 sum 2^(s*scale*log2e))
  *   coef   [h][i]            fp32, signed branch weights (diff: [1, -lambda];
  *                            N-diff: [+l0, -l1, +l2, ...])
@@ -42,7 +43,8 @@
 extern "C" {
 #endif
 
-#define DTA_ABI_VERSION 6   /* 6: obr_dtype (fp16 O_i for 16-bit activations);
+#define DTA_ABI_VERSION 7   /* 7: per-stage backward branch-group caps (group_max_dq, group_max_dkdv);
+                               6: obr_dtype (fp16 O_i for 16-bit activations);
                                5: RoPE of Q_i at the forward's load (rope_freqs, q_rot);
                                4: Obr is fp32 for every dtype; any n_terms >= 1 */
 
@@ -104,7 +106,11 @@ int dta_attn_fwd(const dta_attn_fwd_args* a, void* stream);
  * (SURVEY semantic 5), from which autograd reaches the lambda_q and lambda_k
  * params through get_lambda (diff_transformer.py:41-48).
  * Workspaces (caller-allocated, see dta_attn_bwd_workspace_bytes):
- *   delta   fp32 [i][b][h][t]
+ *   delta   fp32 [i][b][h][t]: PRIVATE to the backward.  The DQ stage writes it in an
+ *           encoding only the DKDV stage of the same call reads (row constants relative
+ *           to each branch group's first branch, re-based in place where the two stages
+ *           group branches differently).  Run DTA_BWD_DQ exactly once per backward and
+ *           DTA_BWD_DKDV after it on the same delta; never read or reuse it otherwise.
  *   dq_f32  optional fp32 [b][t][h][i][d] contiguous: when dq.ptr is NULL the
  *           dQ kernel writes fp32 here instead (callers that post-process dQ,
  *           e.g. the inverse RoPE, keep full precision). */
@@ -138,6 +144,15 @@ typedef struct dta_attn_bwd_args {
                                 query-major kernel adds into dcoef by float atomics */
   uint64_t dropout_seed;     /* the forward's dropout seed */
   int32_t obr_dtype;         /* ABI 6: as dta_attn_fwd_args (the forward's obr) */
+  int32_t group_max_dq;      /* ABI 7, optional (0 = the library's default per stage): the largest
+                                branch group the DQ stage runs as one launch (n_terms above it run
+                                as groups of the largest built branch count <= this cap, one launch
+                                each).  Defaults: 4 for fp32; 16-bit: 2 at head_size 128 and at 64
+                                with n_terms >= 4, else 4.  Setting it to 4 forces every built
+                                native plan (the GPU tests check each one). */
+  int32_t group_max_dkdv;    /* ABI 7, as group_max_dq for the DKDV stage.  Defaults: 4 for fp32;
+                                16-bit: 2 at head_size >= 64, else 4.  Groups after the first
+                                add their dV into the first group's output. */
 } dta_attn_bwd_args;
 
 enum { DTA_BWD_PRE = 1, DTA_BWD_DQ = 2, DTA_BWD_DKDV = 4 };
@@ -272,9 +287,11 @@ const char* dta_error_string(int code);
 int dta_abi_version(void);
 /* 1 if (dtype, head_size, n_terms, dv) runs: an n_terms-branch kernel plan is built for
  * it, or (n_terms >= 2, dv = 2*head_size) the single-branch plan is -- then the forward
- * runs n_terms single-branch workgroups per query block and head plus a combine pass,
- * and the backward runs branch groups of the largest built branch count (<= 4) one after
- * another (dV summed over the groups, d(coef) reduced over all n_terms).  Head sizes
+ * runs n_terms single-branch workgroups per query block and head plus a combine pass.
+ * The backward runs each stage as branch groups of the largest built branch count not
+ * above that stage's cap (group_max_dq / group_max_dkdv and their defaults), one launch
+ * per group (dV summed over the groups, d(coef) reduced over all n_terms); where the two
+ * stages group differently the DQ stage re-bases the delta rows for the DKDV stage.  Head sizes
  * 16, 32, 64, 96, 128 (dv = 2*head_size), and dv = head_size at n_terms = 1 for 32, 64,
  * 96, 128; the Python layer runs other head sizes up to 128 zero-padded to the next one. */
 int dta_supported(int32_t dtype, int32_t head_size, int32_t n_terms, int32_t dv);

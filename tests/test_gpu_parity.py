@@ -68,6 +68,37 @@ CASES = [  # H, N, hs, T, rope
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("H,N,hs,T,rope", CASES)
 def test_core_fwd_bwd(dtype, H, N, hs, T, rope):
+    _core_case(dtype, H, N, hs, T, rope)
+
+
+# Every built native 3- / 4-branch backward plan, forced by ABI 7's per-stage group caps
+# (dta_attn_bwd_args.group_max_dq / group_max_dkdv = 4).  The library's defaults run
+# 16-bit head sizes >= 64 as branch groups of two, so without the caps these plans -- one
+# wave per SIMD, the largest register and LDS footprints -- would go unexercised.
+NATIVE_CASES = [  # H, N, hs, T, rope
+    (1, 3, 128, 130, False), (1, 4, 128, 97, False), (1, 3, 96, 70, True), (1, 4, 96, 100, True),
+    (2, 3, 64, 65, True), (1, 4, 64, 70, False), (2, 3, 32, 200, False), (1, 4, 32, 97, True),
+    (1, 3, 128, 700, True),
+]
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("H,N,hs,T,rope", NATIVE_CASES)
+def test_core_native_backward_plans(dtype, H, N, hs, T, rope):
+    with _ops().bwd_group_caps(4, 4):
+        _core_case(dtype, H, N, hs, T, rope)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_native_hs128_n3_sampled_rows(dtype):
+    """The native 16-bit (hs 128, N 3) backward plans at B=8, H=8, T=4096 (groups forced
+    off): O, dQ, dK, dV, d(coef) on sampled rows of spread (b, h) pairs against fp64."""
+    with _ops().bwd_group_caps(4, 4):
+        _long_case(B=8, H=8, N=3, hs=128, T=4096, pairs=[(0, 0), (7, 7), (3, 5), (5, 2)], n_rows=24,
+                   dtype=dtype, seed=71)
+
+
+def _core_case(dtype, H, N, hs, T, rope):
     ops = _ops()
     from differential_transformer_replication_amd import _lib
     assert _lib.supported(dtype, hs, N, 2 * hs)      # every case runs (natively or in branch groups)

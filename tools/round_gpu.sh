@@ -24,6 +24,8 @@ PC="$PB --no-configs"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 $R/bench.py $PB > $OUT/prof.log 2>&1 || { echo PROF_FAILED; tail -20 $OUT/prof.log; exit 1; }
 head -14 $OUT/prof/run_kernel_stats.csv | cut -c1-200
+# per-(kernel, grid) means: one instance serves several shapes in one bench process
+python3 $R/tools/kernel_stats_by_shape.py $OUT/prof/run_kernel_trace.csv $OUT/kernel_stats_by_shape.csv || exit 1
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- python3 $R/bench.py $PC --steps 3 --warmup 1 > $OUT/pmc_fetch.log 2>&1 || { echo PMC_FETCH_FAILED; tail -5 $OUT/pmc_fetch.log; exit 1; }
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- python3 $R/bench.py $PC --steps 3 --warmup 1 > $OUT/pmc_write.log 2>&1 || { echo PMC_WRITE_FAILED; tail -5 $OUT/pmc_write.log; exit 1; }
 python3 $R/tools/pmc_summary.py $OUT $OUT/pmc_traffic.json B8_H16_hs64_N2_T4096_dv128 || exit 1
