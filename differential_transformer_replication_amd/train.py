@@ -375,8 +375,9 @@ def train_bench(args, world, rank):
            "dtype": "bf16" if cfg.dtype == "bf16" else cfg.dtype, "data": "synthetic", "final_loss": float(loss),
            "config": {"workload": workload, "params": nparams, "micro_batch_per_gpu": cfg.micro_batch_size,
                       "global_batch": cfg.micro_batch_size * world, "seq_len": cfg.block_size,
-                      "parallelism": f"dp{world} (bucketed {'RCCL' if cuda else 'gloo'} all-reduce, "
-                                     f"{cfg.bucket_cap_mb} MB buckets, overlapped with backward)"}}
+                      "parallelism": (f"dp{world} (bucketed {'RCCL' if cuda else 'gloo'} all-reduce, "
+                                      f"{cfg.bucket_cap_mb} MB buckets, overlapped with backward)") if world > 1
+                      else "dp1, no collective (one rank: the bucket all-reduces are not launched)"}}
     if cuda:
         res["model_tflops"] = round(fpt * tps / 1e12, 2)
         res["mfu"] = round(fpt * tps / 1e12 / (world * PEAK_BF16_TFLOPS), 4)
