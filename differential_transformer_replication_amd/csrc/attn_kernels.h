@@ -301,6 +301,26 @@ __device__ __forceinline__ void lgkm_pin_n(lds64 (&r)[M][4]) {
     for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(r[m][j]));
 }
 
+// tr_issue through the compiler's own ds_read_b64_tr_b16 builtin: its waits are the
+// compiler's.  An asm read's destination is "complete" to the compiler the moment the
+// asm issues, so in a plan that spills, the register allocator may store or copy that
+// destination before the data lands (the round-4 non-finite dQ of the 16-bit head size
+// 128 N = 3 plan: 476-508 B/lane of scratch).  Plans that spill read through this
+// instead (the builtin makes the compiler guard it with vmcnt(0), draining the ring's
+// DMA: the cost of correctness there).
+template <int ROWB, int RB, int OFF = 0>
+__device__ __forceinline__ void tr_load(lds64 (&r)[4], unsigned a0, unsigned a1) {
+  typedef short v4s __attribute__((ext_vector_type(4)));
+  auto rd = [](unsigned a) {
+    return __builtin_bit_cast(lds64, __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        reinterpret_cast<__attribute__((address_space(3))) v4s*>((size_t)a)));
+  };
+  r[0] = rd(a0 + OFF + ROWB * RB);
+  r[1] = rd(a1 + OFF + ROWB * (RB + 8));
+  r[2] = rd(a0 + OFF + ROWB * (RB + 16));
+  r[3] = rd(a1 + OFF + ROWB * (RB + 24));
+}
+
 template <class E>
 __device__ __forceinline__ typename Ops<E>::frag tr_frag(const lds64 (&r)[4], int s) {
   typedef short v4s __attribute__((ext_vector_type(4)));
@@ -974,7 +994,9 @@ void attn_fwd_kernel(FwdParams p) {
   // O_i^T += V^T P_i^T, one V fragment feeds every branch
   auto phase_b = [&](int kt, const frag (&pf)[N][NKB * SPB]) {
     const E* Vc = Vb + (kt % NS) * CF::nV;
-    if constexpr (sizeof(E) == 2 && DTA_FWD_PIPE > 0 && NKB == 1 && NDB > 1) {
+    // the dropout plans spill (up to 128 B/lane): compiler-tracked V^T reads (see tr_load)
+    constexpr bool SPILLS = DROP;
+    if constexpr (sizeof(E) == 2 && DTA_FWD_PIPE > 0 && NKB == 1 && NDB > 1 && !SPILLS) {
       // the next d-block's V^T fragments read while this one's MFMAs run (32-key tiles:
       // 8 more VGPRs)
       const unsigned vb = lds_addr(Vc);
@@ -1006,8 +1028,12 @@ void attn_fwd_kernel(FwdParams p) {
         constexpr int d = decltype(D)::value;
         lds64 r[NKB][4];
         const unsigned a0 = vb + (Lv ^ (64 * d)), a1 = vb + (Lv ^ (64 * d + 32));
-        sfor<NKB>([&](auto KB) { tr_issue<VI::ROWB, 32 * decltype(KB)::value>(r[decltype(KB)::value], a0, a1); });
-        lgkm_pin<NKB>(r);
+        if constexpr (SPILLS) {
+          sfor<NKB>([&](auto KB) { tr_load<VI::ROWB, 32 * decltype(KB)::value>(r[decltype(KB)::value], a0, a1); });
+        } else {
+          sfor<NKB>([&](auto KB) { tr_issue<VI::ROWB, 32 * decltype(KB)::value>(r[decltype(KB)::value], a0, a1); });
+          lgkm_pin<NKB>(r);
+        }
 #pragma unroll
         for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
@@ -1245,6 +1271,10 @@ void attn_dq_kernel(BwdParams p) {
 
   // (head size 128 at N >= 3 spills further with the seed fragments: it keeps the fmas)
   constexpr bool SEED = DTA_DQ_SEED && std::is_same<E, __bf16>::value && !DROP && SRD && !(HS >= 128 && N >= 3);
+  // plans that spill (16-bit head size 128 at N >= 3: 84-508 B/lane of scratch; dropout
+  // plans: up to 532 B/lane) read LDS only through compiler-tracked loads: no asm read
+  // whose destination the allocator could spill before it lands (see tr_load)
+  constexpr bool SPILLS = sizeof(E) == 2 && (DROP || (HS >= 128 && N >= 3));
   // ---- per-row operands in registers: Q_i and dO rows (B operands), LSE, delta
   frag qf[NQR > 0 ? NQR : 1][NQR > 0 ? NSQ : 1], df[NSV];
   float coef[N], lse[N], del[N];
@@ -1383,7 +1413,7 @@ void attn_dq_kernel(BwdParams p) {
           const char* vbase = reinterpret_cast<const char*>(Vc);
 #pragma unroll
           for (int kb = 0; kb < NKB; ++kb) dp[kb] = SEED ? O::mma(f_one, f_dp, f32x16{}) : f32x16{};
-          if constexpr (XA && DTA_DQ_PIPE > 0) {
+          if constexpr (XA && DTA_DQ_PIPE > 0 && !SPILLS) {
             // V fragments read DTA_DQ_PIPE MFMAs ahead (k-step major, key block minor)
             constexpr int NIT = NSV * NKB, D = DTA_DQ_PIPE;
             i32x4 vb[D + 1];
@@ -1422,7 +1452,7 @@ void attn_dq_kernel(BwdParams p) {
           constexpr int i = decltype(I_)::value;
           const E* Ki = Kc + i * BN * HSP;
           f32x16 sa[NKB];
-          if constexpr (XA && DTA_DQ_PIPE > 0) {
+          if constexpr (XA && DTA_DQ_PIPE > 0 && !SPILLS) {
             // S'_i chain with its operand reads DTA_DQ_PIPE reads ahead of the MFMAs
             constexpr int QL = i >= NQR ? 1 : 0;
             constexpr int KOFF = i * BN * HSP * (int)sizeof(E), QOFF = (i >= NQR ? i - NQR : 0) * BM * QP * (int)sizeof(E);
@@ -1506,8 +1536,12 @@ void attn_dq_kernel(BwdParams p) {
               const unsigned a0 = XA ? (tK ^ (64 * d)) + (unsigned)(i * BN * HSP * (int)sizeof(E)) : kbse + (Lk ^ (64 * d));
               const unsigned a1 = XA ? (tK ^ (64 * d + 32)) + (unsigned)(i * BN * HSP * (int)sizeof(E))
                                      : kbse + (Lk ^ (64 * d + 32));
-              sfor<NKB>([&](auto KB) { tr_issue<KI::ROWB, 32 * decltype(KB)::value>(r[decltype(KB)::value], a0, a1); });
-              lgkm_pin<NKB>(r);
+              if constexpr (SPILLS) {
+                sfor<NKB>([&](auto KB) { tr_load<KI::ROWB, 32 * decltype(KB)::value>(r[decltype(KB)::value], a0, a1); });
+              } else {
+                sfor<NKB>([&](auto KB) { tr_issue<KI::ROWB, 32 * decltype(KB)::value>(r[decltype(KB)::value], a0, a1); });
+                lgkm_pin<NKB>(r);
+              }
 #pragma unroll
               for (int kb = 0; kb < NKB; ++kb) {
                 dq[i][d] = O::mma(tr_frag<E>(r[kb], 0), O::template pack<0>(sa[kb]), dq[i][d]);
@@ -1716,6 +1750,9 @@ void attn_dkdv_kernel(BwdParams p) {
   constexpr int KS = O::KSTEP;
   constexpr int NSQ = HS / KS, NSV = DV / KS, SPB = 32 / KS;
   constexpr int NHB = (HS + 31) / 32, NVB = DV / 32;
+  // the plans that spill (16-bit head size 128 at N >= 3, the dropout plans: 8-48 VGPRs at
+  // head size 64 N = 2) take compiler-tracked transposed reads (see tr_load)
+  constexpr bool SPILLS = sizeof(E) == 2 && (DROP || (HS >= 128 && N >= 3));
 
   using KI = Img<E, KP>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1964,10 +2001,15 @@ void attn_dkdv_kernel(BwdParams p) {
             lds64 r[NHB][4];
             sfor<NHB>([&](auto D) {
               constexpr int d = decltype(D)::value;
-              if constexpr (XA) tr_issue<QI::ROWB, 0>(r[d], (tQ ^ (64 * d)) + i * RG::QB, (tQ ^ (64 * d + 32)) + i * RG::QB);
-              else tr_issue<QI::ROWB, 0>(r[d], qb + (Lq ^ (64 * d)), qb + (Lq ^ (64 * d + 32)));
+              if constexpr (SPILLS) {
+                if constexpr (XA) tr_load<QI::ROWB, 0>(r[d], (tQ ^ (64 * d)) + i * RG::QB, (tQ ^ (64 * d + 32)) + i * RG::QB);
+                else tr_load<QI::ROWB, 0>(r[d], qb + (Lq ^ (64 * d)), qb + (Lq ^ (64 * d + 32)));
+              } else {
+                if constexpr (XA) tr_issue<QI::ROWB, 0>(r[d], (tQ ^ (64 * d)) + i * RG::QB, (tQ ^ (64 * d + 32)) + i * RG::QB);
+                else tr_issue<QI::ROWB, 0>(r[d], qb + (Lq ^ (64 * d)), qb + (Lq ^ (64 * d + 32)));
+              }
             });
-            lgkm_pin<NHB>(r);
+            if constexpr (!SPILLS) lgkm_pin<NHB>(r);
             const frag p0 = O::template pack<0>(sa), p1 = O::template pack<1>(sa);
 #pragma unroll
             for (int d = 0; d < NHB; ++d) {
@@ -1994,10 +2036,15 @@ void attn_dkdv_kernel(BwdParams p) {
             lds64 r[nb][4];
             sfor<nb>([&](auto E2) {
               constexpr int d = d0 + decltype(E2)::value;
-              if constexpr (XA) tr_issue<DI::ROWB, 0, RG::OFF_D>(r[decltype(E2)::value], tD ^ (64 * d), tD ^ (64 * d + 32));
-              else tr_issue<DI::ROWB, 0>(r[decltype(E2)::value], db + (Ld ^ (64 * d)), db + (Ld ^ (64 * d + 32)));
+              if constexpr (SPILLS) {
+                if constexpr (XA) tr_load<DI::ROWB, 0, RG::OFF_D>(r[decltype(E2)::value], tD ^ (64 * d), tD ^ (64 * d + 32));
+                else tr_load<DI::ROWB, 0>(r[decltype(E2)::value], db + (Ld ^ (64 * d)), db + (Ld ^ (64 * d + 32)));
+              } else {
+                if constexpr (XA) tr_issue<DI::ROWB, 0, RG::OFF_D>(r[decltype(E2)::value], tD ^ (64 * d), tD ^ (64 * d + 32));
+                else tr_issue<DI::ROWB, 0>(r[decltype(E2)::value], db + (Ld ^ (64 * d)), db + (Ld ^ (64 * d + 32)));
+              }
             });
-            lgkm_pin<nb>(r);
+            if constexpr (!SPILLS) lgkm_pin<nb>(r);
 #pragma unroll
             for (int e = 0; e < nb; ++e) {
               dv[d0 + e] = O::mma(tr_frag<E>(r[e], 0), p0, dv[d0 + e]);
