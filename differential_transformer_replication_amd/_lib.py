@@ -26,7 +26,7 @@ EXPORTS = ("dta_attn_fwd", "dta_attn_bwd", "dta_attn_bwd_workspace_bytes", "dta_
            "dta_ln_fwd", "dta_ln_bwd", "dta_ln_bwd_workspace_bytes",
            "dta_rope", "dta_cast_f32", "dta_error_string", "dta_abi_version", "dta_supported",
            "dta_attn_decode", "dta_attn_decode_workspace_bytes", "dta_swiglu_fwd", "dta_swiglu_bwd",
-           "dta_accumulate_f32", "dta_swiglu_bwd_workspace_bytes")
+           "dta_accumulate_f32", "dta_swiglu_bwd_workspace_bytes", "dta_attn_bwd_dkdv_groups")
 
 
 class DtaTensor(ctypes.Structure):
@@ -65,7 +65,8 @@ class AttnBwdArgs(ctypes.Structure):
                 ("dcoef", ctypes.c_void_p), ("delta", ctypes.c_void_p), ("dq_f32", ctypes.c_void_p),
                 ("stages", ctypes.c_int32), ("rope_freqs", ctypes.c_void_p), ("dcoef_partial", ctypes.c_void_p),
                 ("dropout_seed", ctypes.c_uint64), ("obr_dtype", ctypes.c_int32),
-                ("group_max_dq", ctypes.c_int32), ("group_max_dkdv", ctypes.c_int32)]
+                ("group_max_dq", ctypes.c_int32), ("group_max_dkdv", ctypes.c_int32),
+                ("dv_f32", ctypes.c_void_p)]
 
 
 BWD_PRE, BWD_DQ, BWD_DKDV = 1, 2, 4
@@ -140,8 +141,10 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         lib.dta_error_string.argtypes = [ctypes.c_int]
         lib.dta_error_string.restype = ctypes.c_char_p
         lib.dta_supported.argtypes = [ctypes.c_int32] * 4
+        lib.dta_attn_bwd_dkdv_groups.argtypes = [ctypes.c_int32] * 5
         for fn in ("dta_attn_fwd", "dta_attn_bwd", "dta_attn_decode", "dta_ln_fwd", "dta_ln_bwd", "dta_rope", "dta_cast_f32",
-                   "dta_abi_version", "dta_supported", "dta_swiglu_fwd", "dta_swiglu_bwd", "dta_accumulate_f32"):
+                   "dta_abi_version", "dta_supported", "dta_swiglu_fwd", "dta_swiglu_bwd", "dta_accumulate_f32",
+                   "dta_attn_bwd_dkdv_groups"):
             getattr(lib, fn).restype = ctypes.c_int
         if lib.dta_abi_version() != ABI_VERSION:
             raise RuntimeError(f"libdiffattn ABI {lib.dta_abi_version()} != expected {ABI_VERSION}")

@@ -693,6 +693,16 @@ struct FwdCfg {
 };
 
 // NP: no paired plan (the dropout instantiations: their extra registers spill it)
+// Single-branch plans (the branch-split forward's workgroups, the control model) take the
+// paired layout too: Q in registers, 64-key tiles, two 4-wave workgroups per CU instead of
+// one 8-wave workgroup whose SIMD partners run in lockstep.  One-process A/B
+// (profiles/r05c_ab_pair_n1.json, outputs bitwise equal): cfg3 N = 3 forward 0.398 ->
+// 0.369 ms, N = 4 0.506 -> 0.484; control hs 64 forward 0.222 -> 0.199, dQ 0.273 -> 0.252;
+// control hs 128 (cfg5) dQ 11.36 -> 10.73 ms but forward 8.60 -> 8.79, so the head size 128
+// forward keeps the 8-wave plan.  DTA_PAIR_N1 = 0 (A/B builds) keeps 8 waves everywhere.
+#ifndef DTA_PAIR_N1
+#define DTA_PAIR_N1 1
+#endif
 template <class E, int HS, int N, int DV = 2 * HS, bool NP = false>
 struct FwdPick {
   static constexpr int DVC = FwdChunk<N, DV, sizeof(E) == 2>::DVC;
@@ -704,7 +714,7 @@ struct FwdPick {
                              FwdCfg<E, HS, N, DVC, 8, false>::regs <= 280;
   static constexpr bool q4 = FwdCfg<E, HS, N, DVC, 4, false>::bytes <= LIM;
   // paired 4-wave plan with 64-key tiles and branch 0's Q in registers
-  static constexpr int QRH = (q8 && N >= 2 &&
+  static constexpr int QRH = (q8 && (N >= 2 || (DTA_PAIR_N1 && HS <= 96)) &&
                               FwdCfg<E, HS, N, DVC, 4, false, 1>::bytes <= 80 * 1024) ? 1 : 0;
   static constexpr bool pair = !NP && QRH == 1 && q8 &&
                                 FwdCfg<E, HS, N, DVC, 4, false, QRH>::PAIR &&
@@ -715,7 +725,11 @@ struct FwdPick {
   static constexpr bool ok = FwdCfg<E, HS, N, DVC, NW, QREG, QH>::bytes <= LIM;
 };
 
-template <class E, int HS, int N, int DVC, int NW, bool QREG, bool SRD, bool DROP, int QRH>
+// SEQ (N = 1 paired plans only): the workgroup runs p.bseq branches one after another over
+// the same query block -- each branch's key loop, O_i and LSE_i as a branch-split
+// workgroup would -- and keeps O = sum_i c_i O_i in registers across them, so the
+// branch-split forward needs no combine pass (see launch_fwd_t).
+template <class E, int HS, int N, int DVC, int NW, bool QREG, bool SRD, bool DROP, int QRH, bool SEQ = false>
 __global__ __launch_bounds__(NW * 64, (FwdCfg<E, HS, N, DVC, NW, QREG, QRH>::PAIR ? 2 : FwdCfg<E, HS, N, DVC, NW, QREG, QRH>::WPE))
 void attn_fwd_kernel(FwdParams p) {
   using O = Ops<E>;
@@ -759,14 +773,31 @@ void attn_fwd_kernel(FwdParams p) {
   const int q0 = qt * BM, qw0 = q0 + wave * 32;
   int qrow = qw0 + c32;
 
+  static_assert(!SEQ || (N == 1 && QRH == 1 && DVC == 2 * HS && !DROP), "SEQ: N = 1 paired plans, whole dv");
+  const int nseq = SEQ ? p.bseq : 1;
   const E* gq = reinterpret_cast<const E*>(p.q.p) + b * p.q.sb + hh * p.q.sh + br * p.q.si;
   const E* gk = reinterpret_cast<const E*>(p.k.p) + b * p.k.sb + hh * p.k.sh + br * p.k.si;
   const E* gv = reinterpret_cast<const E*>(p.v.p) + b * p.v.sb + hh * p.v.sh + dc0;
+  const bool qrope = p.rope != nullptr;
+  E* gqr = qrope ? reinterpret_cast<E*>(p.qrot.p) + b * p.qrot.sb + hh * p.qrot.sh + br * p.qrot.si : nullptr;
 
   float coef[N];
 #pragma unroll
   for (int i = 0; i < N; ++i) coef[i] = nsp > 1 ? 1.f : p.coef[hh * p.cst + i];
+  constexpr int NDBS = SEQ ? DVC / 32 : 1;
+  f32x16 oacc[NDBS];                  // SEQ: sum_i c_i O_i over the branches done so far
+#pragma unroll
+  for (int d = 0; d < NDBS; ++d) oacc[d] = f32x16{};
 
+  for (int sb = 0; sb < nseq; ++sb) {
+  if constexpr (SEQ) {
+    if (sb > 0) {
+      gq += p.q.si; gk += p.k.si;
+      if (qrope) gqr += p.qrot.si;
+    }
+    coef[0] = p.coef[hh * p.cst + sb];
+  }
+  const int brs = SEQ ? sb : br;      // this pass's branch index (LSE_i / O_i rows)
   frag qf[NQR > 0 ? NQR : 1][NQR > 0 ? NSQ : 1];
 #pragma unroll
   for (int i = 0; i < NQR; ++i)
@@ -780,8 +811,6 @@ void attn_fwd_kernel(FwdParams p) {
   // RoPE at load (p.rope, ABI 5): Q_i arrive un-rotated; the rows in registers turn here,
   // the LDS-staged ones once they land (first attempt); each rotated row is stored once to
   // p.qrot for the backward (by the dv chunk 0 workgroup), so the RoPE pass rotates K only
-  const bool qrope = p.rope != nullptr;
-  E* gqr = qrope ? reinterpret_cast<E*>(p.qrot.p) + b * p.qrot.sb + hh * p.qrot.sh + br * p.qrot.si : nullptr;
   bool qrot_pending = qrope && N > NQR;
   if (qrope) {
     const int tr = min(qrow, T - 1);
@@ -1138,19 +1167,20 @@ void attn_fwd_kernel(FwdParams p) {
   st.lap<5>();
   st.flush(p.stamps, lin * NW + wave, lane);
 
-  if (!wave_live || qrow >= T) return;
+  if (!SEQ && (!wave_live || qrow >= T)) return;
+  if (wave_live && qrow < T) {      // (SEQ: every lane stays for the next branch's barriers)
   float inv[N];
 #pragma unroll
   for (int i = 0; i < N; ++i) {
     const float lt = wave_sum_halves(l[i]);
     inv[i] = 1.f / lt;
     if (dc0 == 0 && hf == 0)
-      p.lse[(((int64_t)(br + i) * p.B + b) * p.H + hh) * T + qrow] = -(m[i] + __builtin_log2f(lt));   // stored negated
+      p.lse[(((int64_t)(brs + i) * p.B + b) * p.H + hh) * T + qrow] = -(m[i] + __builtin_log2f(lt));   // stored negated
   }
   E* go = reinterpret_cast<E*>(p.o.p) + b * p.o.sb + (int64_t)qrow * p.o.st + hh * p.o.sh + dc0;
   // O_i saved for the backward's delta_i = <dO, O_i> (whose sums feed d(lambda)): fp32, or
   // fp16 (p.ob16: 2^-11, eight times bf16's resolution, half the bytes)
-  const int64_t gob = b * p.obr.sb + (int64_t)qrow * p.obr.st + hh * p.obr.sh + br * p.obr.si + dc0;
+  const int64_t gob = b * p.obr.sb + (int64_t)qrow * p.obr.st + hh * p.obr.sh + brs * p.obr.si + dc0;
 #pragma unroll
   for (int d = 0; d < NDB; ++d)
 #pragma unroll
@@ -1165,8 +1195,24 @@ void attn_fwd_kernel(FwdParams p) {
         o0 = fmaf(coef[i], a0, o0); o1 = fmaf(coef[i], a1, o1);
         o2 = fmaf(coef[i], a2, o2); o3 = fmaf(coef[i], a3, o3);
       }
-      if (nsp == 1) store4<E>(go + e, o0, o1, o2, o3);
+      if constexpr (SEQ) {
+        oacc[d < NDBS ? d : 0][4 * g + 0] += o0; oacc[d < NDBS ? d : 0][4 * g + 1] += o1;
+        oacc[d < NDBS ? d : 0][4 * g + 2] += o2; oacc[d < NDBS ? d : 0][4 * g + 3] += o3;
+      } else {
+        if (nsp == 1) store4<E>(go + e, o0, o1, o2, o3);
+      }
     }
+  }
+  }   // branches (SEQ)
+  if constexpr (SEQ) {
+    if (qw0 >= T || qrow >= T) return;
+    E* go = reinterpret_cast<E*>(p.o.p) + b * p.o.sb + (int64_t)qrow * p.o.st + hh * p.o.sh + dc0;
+#pragma unroll
+    for (int d = 0; d < NDBS; ++d)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        store4<E>(go + d * 32 + 8 * g + 4 * hf, oacc[d][4 * g], oacc[d][4 * g + 1], oacc[d][4 * g + 2], oacc[d][4 * g + 3]);
+  }
 }
 
 // ------------------------------------------------------ backward: dQ ---
@@ -1194,7 +1240,7 @@ struct DqPick {
   static constexpr int LIM = 160 * 1024;
   static constexpr bool q8 = sizeof(E) == 2 && DqCfg<E, HS, N, DV, 8, false>::bytes <= LIM;
   // paired 4-wave plan with 64-key tiles and branch 0's Q in registers
-  static constexpr int QRH = (q8 && N >= 2 &&
+  static constexpr int QRH = (q8 && (N >= 2 || DTA_PAIR_N1) &&
                               DqCfg<E, HS, N, DV, 4, false, 1>::bytes <= 80 * 1024) ? 1 : 0;
   // (head size >= 64: the hs = 32, N = 3 paired plan spills)
   static constexpr bool pair = !NP && QRH == 1 && q8 && HS >= 64 &&
@@ -2101,6 +2147,10 @@ void attn_dkdv_kernel(BwdParams p) {
   }
   if constexpr (DVV) {
     E* gdv = reinterpret_cast<E*>(p.dv.p) + b * p.dv.sb + (int64_t)krow * p.dv.st + hh * p.dv.sh;
+    // branch groups with an fp32 dV workspace (dv32): every group but the last keeps the
+    // running sum there, the last adds it and does the only rounding to E
+    float* g32 = p.dv32 ? p.dv32 + (((int64_t)b * p.T + krow) * p.H + hh) * p.DV : nullptr;
+    const bool to32 = g32 != nullptr && !p.dv_last;
 #pragma unroll
     for (int d = 0; d < NVB; ++d)
 #pragma unroll
@@ -2108,9 +2158,15 @@ void attn_dkdv_kernel(BwdParams p) {
         const int e = d * 32 + 8 * g + 4 * hf;
         float a0 = dv[d][4 * g], a1 = dv[d][4 * g + 1], a2 = dv[d][4 * g + 2], a3 = dv[d][4 * g + 3];
         if (p.dv_acc) {        // a later branch group: dV = sum over every group's branches
-          a0 += (float)gdv[e]; a1 += (float)gdv[e + 1]; a2 += (float)gdv[e + 2]; a3 += (float)gdv[e + 3];
+          if (g32) {
+            const f32x4 v = *reinterpret_cast<const f32x4*>(g32 + e);
+            a0 += v[0]; a1 += v[1]; a2 += v[2]; a3 += v[3];
+          } else {
+            a0 += (float)gdv[e]; a1 += (float)gdv[e + 1]; a2 += (float)gdv[e + 2]; a3 += (float)gdv[e + 3];
+          }
         }
-        store4<E>(gdv + e, a0, a1, a2, a3);
+        if (to32) store4<float>(g32 + e, a0, a1, a2, a3);
+        else store4<E>(gdv + e, a0, a1, a2, a3);
       }
   }
 }
@@ -2186,6 +2242,20 @@ __global__ __launch_bounds__(256) void branch_combine_kernel(FwdParams p, Combin
 #ifndef DTA_FWD_BSPLIT
 #define DTA_FWD_BSPLIT -1
 #endif
+// Sequential-branch forward (SEQ kernels): where the N-branch forward runs branch-split and
+// the single-branch plan is the paired one with the whole dv in one workgroup, the N
+// branches of a query block run one after another in one workgroup, which forms O itself
+// instead of a combine pass re-reading every fp32 O_i (DTA_FWD_SEQ = 0 in A/B builds: the
+// branch-split workgroups plus branch_combine_kernel).
+#ifndef DTA_FWD_SEQ
+#define DTA_FWD_SEQ 1
+#endif
+template <class E, int HS, int DV, bool DROP>
+constexpr bool fwd_seq_ok() {
+  return DTA_FWD_SEQ && !DROP && sizeof(E) == 2 && DV == 2 * HS && FwdPick<E, HS, 1, DV, DROP>::pair &&
+         FwdPick<E, HS, 1, DV, DROP>::DVC == DV;
+}
+
 template <class E, int HS, int N, int DV_ = 2 * HS>
 struct Plan {
   static constexpr int DV = DV_;
@@ -2214,6 +2284,10 @@ int launch_fwd_t(const FwdParams& p, hipStream_t st) {
   if constexpr (CAN) {
     if (AUTO || DTA_FWD_BSPLIT > 0) {
       FwdParams q = p;
+      if constexpr (fwd_seq_ok<E, HS, PL::DV, DROP>()) {
+        q.bseq = N;
+        return launch_fwd_t<E, HS, 1, DV_, DROP>(q, st);
+      }
       q.bsplit = N;
       if (int e = launch_fwd_t<E, HS, 1, DV_, DROP>(q, st)) return e;
       const int64_t n = (int64_t)p.B * p.T * p.H * (PL::DV / (16 / (int)sizeof(E)));
@@ -2229,10 +2303,14 @@ int launch_fwd_t(const FwdParams& p, hipStream_t st) {
   const int nsp = (N == 1 && p.bsplit > 1) ? p.bsplit : 1;
   dim3 grid((p.T + NW * 32 - 1) / (NW * 32), p.H * nsp * (PL::DV / DVC), p.B);
   auto run = [&](auto SRDV) -> int {
-    auto kern = attn_fwd_kernel<E, HS, N, DVC, NW, FP::QREG, decltype(SRDV)::value, DROP, QH>;
-    if (int e = set_smem(kern, bytes)) return e;
-    hipLaunchKernelGGL(kern, grid, dim3(NW * 64), bytes, st, p);
-    return 0;
+    auto go = [&](auto K) -> int {
+      if (int e = set_smem(K, bytes)) return e;
+      hipLaunchKernelGGL(K, grid, dim3(NW * 64), bytes, st, p);
+      return 0;
+    };
+    if constexpr (N == 1 && fwd_seq_ok<E, HS, PL::DV, DROP>())
+      if (p.bseq > 1) return go(attn_fwd_kernel<E, HS, N, DVC, NW, FP::QREG, decltype(SRDV)::value, DROP, QH, true>);
+    return go(attn_fwd_kernel<E, HS, N, DVC, NW, FP::QREG, decltype(SRDV)::value, DROP, QH>);
   };
   int e = 0;
   if constexpr (KvRing<E, HS, N, DVC, FwdCfg<E, HS, N, DVC, NW, FP::QREG, QH>::BN, NW>::ok)
@@ -2341,12 +2419,15 @@ int fwd_branch_split_any(const FwdParams& p, hipStream_t st) {
   FwdParams q = p;
   q.bsplit = p.N;
   int e = -2;
+  bool seq = false;
 #define DTA_F1(HS_, N_, DV_) \
   if (N_ == 1 && p.HS == HS_ && p.DV == DV_) { \
-    if constexpr (N_ == 1 && Plan<E, HS_, 1, DV_>::ok) e = launch_fwd_t<E, HS_, 1, DV_, DROP>(q, st); }
+    if constexpr (N_ == 1 && Plan<E, HS_, 1, DV_>::ok) { \
+      if constexpr (fwd_seq_ok<E, HS_, DV_, DROP>()) { q.bsplit = 0; q.bseq = p.N; seq = true; } \
+      e = launch_fwd_t<E, HS_, 1, DV_, DROP>(q, st); } }
   DTA_FOR_CONFIGS(DTA_F1)
 #undef DTA_F1
-  if (e) return e;
+  if (e || seq) return e;
   const int64_t n = (int64_t)p.B * p.T * p.H * (p.DV / (16 / (int)sizeof(E)));
   if (n >= (1ll << 31)) return -2;
   hipLaunchKernelGGL((branch_combine_kernel<E, 0>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, p,

@@ -245,6 +245,16 @@ int dta_attn_fwd(const dta_attn_fwd_args* a, void* stream) {
   return status(launch_attn_fwd(a->dtype, p, (hipStream_t)stream));
 }
 
+// dK/dV launches (branch groups) a backward of this shape runs at the default caps: more than
+// one means dV is summed across groups (in dv_f32 when given)
+int dta_attn_bwd_dkdv_groups(int32_t dtype, int32_t head_size, int32_t n_terms, int32_t dv, int32_t group_max_dkdv) {
+  if (!attn_supported(dtype, head_size, n_terms, dv)) return 0;
+  const int cap = group_max_dkdv > 0 ? group_max_dkdv : bwd_group_cap(dtype, head_size, n_terms, true);
+  int n = 0;
+  for (int g0 = 0, ng; g0 < n_terms; g0 += ng, ++n) ng = branch_group(dtype, head_size, n_terms - g0, dv, cap);
+  return n;
+}
+
 size_t dta_attn_bwd_dcoef_partial_bytes(int32_t B, int32_t T, int32_t H, int32_t n_terms) {
   return (size_t)H * n_terms * B * ((T + 31) / 32) * 4;
 }
@@ -283,6 +293,7 @@ int dta_attn_bwd(const dta_attn_bwd_args* a, void* stream) {
   if (a->rope_freqs && (a->head_size % 4 || reinterpret_cast<uintptr_t>(a->rope_freqs) % 16)) return DTA_ERR_INVALID;
   p.rope = a->rope_freqs;
   if (a->dcoef_partial && !aligned_ptr(a->dcoef_partial)) return DTA_ERR_INVALID;
+  if (a->dv_f32 && !aligned_ptr(a->dv_f32)) return DTA_ERR_INVALID;
   p.dcoef_part = a->dcoef_partial;
   p.B = a->B; p.T = a->T; p.H = a->H; p.N = a->n_terms; p.HS = a->head_size; p.DV = a->dv;
   p.scale = a->scale; p.sl2 = a->scale * kLog2e;
@@ -302,7 +313,7 @@ int dta_attn_bwd(const dta_attn_bwd_args* a, void* stream) {
     if (q.dq32) q.dq32 += (int64_t)g0 * p.HS;
     q.lse += g0 * rowvec; q.delta += g0 * rowvec; q.coef += g0; q.dcoef += g0;
     if (q.dcoef_part) q.dcoef_part += g0 * (int64_t)p.B * nblk;
-    q.N = ng; q.br0 = g0; q.dv_acc = g0 > 0;
+    q.N = ng; q.br0 = g0; q.dv_acc = g0 > 0; q.dv_last = g0 + ng == p.N;
     return q;
   };
   int e = 0;
@@ -328,9 +339,13 @@ int dta_attn_bwd(const dta_attn_bwd_args* a, void* stream) {
       return status(e);
   }
   if (stages & DTA_BWD_DKDV) {
+    // more than one dK/dV group: dV is summed in the fp32 workspace when the caller gave one
+    const bool multi = branch_group(a->dtype, p.HS, p.N, p.DV, kcap) < p.N;
     for (int g0 = 0, ng; g0 < p.N; g0 += ng) {
       ng = branch_group(a->dtype, p.HS, p.N - g0, p.DV, kcap);
-      if ((e = launch_attn_dkdv(a->dtype, group(g0, ng), st))) return status(e);
+      BwdParams q = group(g0, ng);
+      q.dv32 = multi ? a->dv_f32 : nullptr;
+      if ((e = launch_attn_dkdv(a->dtype, q, st))) return status(e);
     }
   }
   return DTA_OK;

@@ -23,6 +23,8 @@ struct FwdParams {
   uint32_t drop_seed_lo, drop_seed_hi;
   int bsplit;          // launcher-internal: > 1 = branch-split launch of the N = 1 kernel
                        // (one branch of bsplit per workgroup; writes O_i and LSE_i only)
+  int bseq;            // launcher-internal: > 1 = the N = 1 kernel runs bseq branches one after
+                       // another per workgroup and writes O as well (no combine pass)
   int cst;             // row stride of coef [h][cst] (the call's total branch count)
   const float* rope;   // if set (ABI 5): q is un-rotated; the forward rotates Q_i at load
   T5 qrot;             //   (fp32 [T][HS/2][2] table) and stores the rotated rows here
@@ -51,6 +53,8 @@ struct BwdParams {
                        // [h][cst], of the d(coef) partials and of dq32; dropout's branch index
   int br0;             // the group's first branch (dropout mask key)
   int dv_acc;          // dK/dV kernel: add into dv instead of storing (groups after the first)
+  float* dv32;         // optional fp32 [b][t][h][e] running dV sum across branch groups
+  int dv_last;         // the last dK/dV group (with dv32: the one that writes dv)
   int ob16;            // obr holds fp16 O_i (ABI 6)
 };
 

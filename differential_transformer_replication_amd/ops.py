@@ -205,6 +205,10 @@ class _DiffAttention(torch.autograd.Function):
         delta = torch.empty(N, B, H, T, device=dev, dtype=torch.float32)
         # d(coef) from per-wave partials summed in a fixed order: reproducible lambda grads
         dcp = torch.empty(lib.dta_attn_bwd_dcoef_partial_bytes(B, T, H, N) // 4, device=dev, dtype=torch.float32)
+        # dK/dV in more than one branch group: dV summed in fp32 across the groups (one rounding)
+        dv32 = None
+        if dt != _lib.DTA_F32 and lib.dta_attn_bwd_dkdv_groups(dt, hs, N, dv, _BWD_GROUP_MAX[1]) > 1:
+            dv32 = torch.empty(B, T, H, dv, device=dev, dtype=torch.float32)
         # with RoPE the kernels differentiate w.r.t. the rotated Q/K (qk_rot) and their
         # dQ / dK epilogues apply the inverse rotation, writing straight into dqkv
         obr_t = _lib.DtaTensor(obr.data_ptr(), *obr.stride()[1:4], obr.stride(0))
@@ -214,7 +218,8 @@ class _DiffAttention(torch.autograd.Function):
                              _lib.tensor5(dq), _lib.tensor5(dk), _lib.tensor5(dvv),
                              dcoef.data_ptr(), delta.data_ptr(), None, _lib.BWD_PRE,
                              freqs.data_ptr() if freqs is not None else None, dcp.data_ptr(), ctx.drop[1],
-                             _lib.dtype_code(obr.dtype), *_BWD_GROUP_MAX)
+                             _lib.dtype_code(obr.dtype), *_BWD_GROUP_MAX,
+                             dv32.data_ptr() if dv32 is not None else None)
         _lib.check(lib.dta_attn_bwd(a, stream))
         a.stages = _lib.BWD_DQ
         with TIMER.region("attn_bwd_dq"):

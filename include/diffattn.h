@@ -152,7 +152,12 @@ typedef struct dta_attn_bwd_args {
                                 native plan (the GPU tests check each one). */
   int32_t group_max_dkdv;    /* ABI 7, as group_max_dq for the DKDV stage.  Defaults: 4 for fp32;
                                 16-bit: 2 at head_size >= 64, else 4.  Groups after the first
-                                add their dV into the first group's output. */
+                                add their dV into the first group's. */
+  float* dv_f32;             /* ABI 7, optional fp32 workspace [b][t][h][e] contiguous (B*T*H*dv
+                                floats, 16-byte aligned): where the DKDV stage runs more than one
+                                group (dta_attn_bwd_dkdv_groups > 1), the running dV sum stays here
+                                in fp32 and only the last group rounds it to dtype.  NULL: each later
+                                group adds into dv_out (one extra 16-bit rounding per group). */
 } dta_attn_bwd_args;
 
 enum { DTA_BWD_PRE = 1, DTA_BWD_DQ = 2, DTA_BWD_DKDV = 4 };
@@ -161,6 +166,9 @@ int dta_attn_bwd(const dta_attn_bwd_args* a, void* stream);
 size_t dta_attn_bwd_workspace_bytes(int32_t B, int32_t T, int32_t H, int32_t n_terms,
                                     int32_t head_size);
 size_t dta_attn_bwd_dcoef_partial_bytes(int32_t B, int32_t T, int32_t H, int32_t n_terms);
+/* The number of dK/dV launches (branch groups) dta_attn_bwd runs for this shape with the given
+ * group_max_dkdv (0 = default); 0 if the shape is unsupported.  > 1: pass dv_f32. */
+int dta_attn_bwd_dkdv_groups(int32_t dtype, int32_t head_size, int32_t n_terms, int32_t dv, int32_t group_max_dkdv);
 
 /* Cross-head LayerNorm x out_scale (GroupLayerNorm.forward,
  * diff_transformer.py:15-20, then `out * (1 - self.lambda_init)`,

@@ -41,9 +41,10 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--obr", choices=["f32", "f16"], default="f32", help="O_i storage (ABI 6 obr_dtype)")
+    ap.add_argument("--dv", type=int, default=0, help="value width (default 2 * head size; head size for N = 1 control)")
     args = ap.parse_args()
     B, H, hs, N, T = (int(x) for x in args.shape.split(","))
-    dv = 2 * hs
+    dv = args.dv or 2 * hs
     dev = torch.device("cuda", 0)
     builds = []
     for b in args.builds:
