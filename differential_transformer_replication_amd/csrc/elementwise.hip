@@ -784,14 +784,32 @@ __global__ __launch_bounds__(256) void swiglu_bwd_bias_kernel(SwigluParams p, fl
   st8<float>(pa, sa);
   st8<float>(pa + p.n, sb);
 }
-__global__ __launch_bounds__(256) void swiglu_bias_reduce_kernel(const float* part, int nblk, int64_t n2, float* out) {
+// the column sums of the nblk partial rows, in a fixed order, in two passes: pass 1 sums each
+// of kSwChunks contiguous runs of partial rows (every load of a run in flight together),
+// pass 2 adds the run sums in order.  (One pass with one thread per column walked all
+// 256 partial rows of cfg4 serially: 98 us per call, latency-bound.)
+constexpr int kSwChunks = 16;
+__global__ __launch_bounds__(256) void swiglu_bias_reduce1_kernel(const float* part, int nblk, int64_t n2, float* part2) {
+  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j >= n2) return;
+  const int per = (nblk + kSwChunks - 1) / kSwChunks;
+  const int b0 = blockIdx.y * per, b1 = min(nblk, b0 + per);
+  float s = 0.f;
+#pragma unroll 16
+  for (int b = b0; b < b1; ++b) s += part[(int64_t)b * n2 + j];
+  part2[(int64_t)blockIdx.y * n2 + j] = s;
+}
+__global__ __launch_bounds__(256) void swiglu_bias_reduce_kernel(const float* part2, int64_t n2, float* out) {
   const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (j >= n2) return;
   float s = 0.f;
-  for (int b = 0; b < nblk; ++b) s += part[(int64_t)b * n2 + j];
+#pragma unroll
+  for (int c = 0; c < kSwChunks; ++c) s += part2[(int64_t)c * n2 + j];
   out[j] = s;
 }
-int64_t swiglu_bias_work_floats(int64_t rows, int64_t n) { return (rows + SWIGLU_RB - 1) / SWIGLU_RB * 2 * n; }
+int64_t swiglu_bias_work_floats(int64_t rows, int64_t n) {
+  return ((rows + SWIGLU_RB - 1) / SWIGLU_RB + kSwChunks) * 2 * n;
+}
 
 int launch_swiglu_bias(int dtype, const SwigluParams& p, float* dbias, float* work, hipStream_t st) {
   const int nblk = (int)((p.rows + SWIGLU_RB - 1) / SWIGLU_RB);
@@ -802,8 +820,10 @@ int launch_swiglu_bias(int dtype, const SwigluParams& p, float* dbias, float* wo
     case 2: hipLaunchKernelGGL(swiglu_bwd_bias_kernel<float>, g, dim3(256), 0, st, p, work); break;
     default: return -1;
   }
-  hipLaunchKernelGGL(swiglu_bias_reduce_kernel, dim3((unsigned)((2 * p.n + 255) / 256)), dim3(256), 0, st, work, nblk,
-                     2 * p.n, dbias);
+  float* part2 = work + (int64_t)nblk * 2 * p.n;
+  const unsigned gx = (unsigned)((2 * p.n + 255) / 256);
+  hipLaunchKernelGGL(swiglu_bias_reduce1_kernel, dim3(gx, kSwChunks), dim3(256), 0, st, work, nblk, 2 * p.n, part2);
+  hipLaunchKernelGGL(swiglu_bias_reduce_kernel, dim3(gx), dim3(256), 0, st, part2, 2 * p.n, dbias);
   return (int)hipGetLastError();
 }
 
