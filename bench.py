@@ -465,9 +465,8 @@ def hbm_bench(reps=20):
     ba = _lib.LnArgs(_lib.DTA_BF16, rows, C, 1e-5, 0.2, x.data_ptr(), C, None, 0, w.data_ptr(), None,
                      mean.data_ptr(), rstd.data_ptr(), dy.data_ptr(), C, dx.data_ptr(), C, dw.data_ptr(),
                      db.data_ptr(), part.data_ptr())
-    ba.ticket = _lib.ln_ticket(dev).data_ptr()     # ABI 7: the ordered dw/db reduce inside the kernel
     ms_f = timed(lambda: _lib.check(lib.dta_ln_fwd(fa, stream)))
-    # the production backward: ln_bwd with the ordered reduce of its column partials folded in (dw/db accumulate: values unused)
+    # the production backward: ln_bwd + the ordered reduce of its column partials (dw/db accumulate: values unused)
     ms_b = timed(lambda: _lib.check(lib.dta_ln_bwd(ba, stream)))
     for name, ms, nbytes in (("ln_fwd", ms_f, 2 * rows * C * 2), ("ln_bwd", ms_b, 3 * rows * C * 2)):
         out[name] = {"us": round(ms * 1e3, 2), "alg_bytes": nbytes, "GBps": round(nbytes / ms / 1e6, 1),

@@ -84,7 +84,7 @@ class LnArgs(ctypes.Structure):
                 ("dw", ctypes.c_void_p), ("db", ctypes.c_void_p), ("partial", ctypes.c_void_p), ("io_dtype", ctypes.c_int32),
                 ("res", ctypes.c_void_p), ("res_stride", ctypes.c_int64), ("xo", ctypes.c_void_p),
                 ("xo_stride", ctypes.c_int64), ("dres", ctypes.c_void_p), ("dres_stride", ctypes.c_int64),
-                ("dx16", ctypes.c_void_p), ("dx16_stride", ctypes.c_int64), ("ticket", ctypes.c_void_p)]
+                ("dx16", ctypes.c_void_p), ("dx16_stride", ctypes.c_int64)]
 
 
 class RopeArgs(ctypes.Structure):
@@ -104,18 +104,6 @@ class DecodeArgs(ctypes.Structure):
 
 _lock = threading.Lock()
 _lib: Optional[ctypes.CDLL] = None
-
-
-_TICKETS = {}
-
-
-def ln_ticket(device) -> torch.Tensor:
-    """The per-device ticket counters of dta_ln_bwd's in-kernel dw / db reduce (ABI 7):
-    zeroed once, left zero by every call.  Backward passes run on one stream in order."""
-    t = _TICKETS.get(device)
-    if t is None:
-        t = _TICKETS[device] = torch.zeros(64, device=device, dtype=torch.int32)
-    return t
 
 
 def load(path: str = LIB_PATH) -> ctypes.CDLL:

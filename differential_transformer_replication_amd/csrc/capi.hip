@@ -368,7 +368,6 @@ static int ln_common(const dta_ln_args* a, bool bwd) {
     return DTA_ERR_INVALID;
   if (bwd && a->dres && (!aligned_ptr(a->dres) || a->dres_stride % v)) return DTA_ERR_INVALID;
   if (bwd && a->dx16 && (!aligned_ptr(a->dx16) || a->dx16_stride % v)) return DTA_ERR_INVALID;
-  if (bwd && a->ticket && !a->partial) return DTA_ERR_INVALID;
   return DTA_OK;
 }
 
@@ -382,7 +381,6 @@ static LnParams ln_params(const dta_ln_args* a) {
   p.partial = a->partial;
   p.res = a->res; p.ress = a->res_stride; p.xo = a->xo; p.xos = a->xo_stride;
   p.dres = a->dres; p.dress = a->dres_stride; p.dx16 = a->dx16; p.dx16s = a->dx16_stride;
-  p.ticket = a->ticket;
   return p;
 }
 

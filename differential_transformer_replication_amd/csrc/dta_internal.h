@@ -85,8 +85,6 @@ struct LnParams {
   float* xo; int64_t xos;          // ... and written here (fp32)
   const float* dres; int64_t dress;  // bwd: dx += dres (the residual branch's gradient)
   void* dx16; int64_t dx16s;       // bwd: dx also stored in y's dtype
-  unsigned* ticket;    // bwd, with partial: the ordered dw / db reduce inside the kernel
-                       // (kLnChunks + 1 counters, zero on entry, left zero)
 };
 int launch_ln_mixed(int y_dtype, const LnParams& p, bool bwd, hipStream_t st);   // x fp32, y / dy 16-bit
 int ln_bwd_blocks(int64_t rows);

@@ -278,57 +278,6 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnParams p) {
 #ifndef DTA_LN_BWD_RPI
 #define DTA_LN_BWD_RPI 1         // rows per barrier (each workgroup step)
 #endif
-constexpr int kLnChunks = 32;    // runs of partial rows in the ordered dw / db reduce
-
-// One release / count hand-off of a workgroup's plain stores (MI355X_MICROARCH.md, valid
-// forms: every storing wave drains with vmcnt(0), workgroup barrier, one lane releases at
-// agent scope and counts; the counter's returned value is the poll, then one agent
-// acquire).  Returns, in every thread, whether this workgroup was the last of `total`.
-__device__ __forceinline__ bool ln_ticket(unsigned* ctr, unsigned total, int t) {
-  __shared__ int last;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (t == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned old = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = old == total - 1;
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-  }
-  __syncthreads();
-  return last != 0;
-}
-
-// The ordered dw / db reduce inside the backward kernel (p.ticket): the last workgroup of
-// each run of `per` blocks sums the run's partial rows in block order (ln_bwd_reduce1),
-// the last run-summer adds the run sums in run order into dw / db (ln_bwd_reduce2) and
-// zeroes the tickets for the next call -- the same association, so the same bits, as
-// the two reduce launches it replaces.
-__device__ void ln_bwd_fold(const LnParams& p, int t) {
-  const int nblk = gridDim.x;
-  const int per = (nblk + kLnChunks - 1) / kLnChunks, ng = (nblk + per - 1) / per;
-  const int grp = blockIdx.x / per, b0 = grp * per, gsz = min(per, nblk - b0);
-  const int64_t n2 = 2 * p.C;
-  float* gsum = p.partial + (int64_t)nblk * n2;         // [kLnChunks][2][C]
-  if (!ln_ticket(p.ticket + grp, (unsigned)gsz, t)) return;
-  for (int64_t e = (int64_t)t * 4; e < n2; e += 256 * 4) {
-    f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int b = b0; b < b0 + gsz; ++b) s += *reinterpret_cast<const f32x4*>(p.partial + (int64_t)b * n2 + e);
-    *reinterpret_cast<f32x4*>(gsum + (int64_t)grp * n2 + e) = s;
-  }
-  if (!ln_ticket(p.ticket + kLnChunks, (unsigned)ng, t)) return;
-  for (int64_t e = (int64_t)t * 4; e < n2; e += 256 * 4) {
-    f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int g = 0; g < ng; ++g) s += *reinterpret_cast<const f32x4*>(gsum + (int64_t)g * n2 + e);
-    float* d = e < p.C ? p.dw + e : p.db + (e - p.C);     // C % 8 == 0: 4 columns never straddle
-#pragma unroll
-    for (int j = 0; j < 4; ++j) d[j] += s[j];             // (dw / db need only 4-byte alignment)
-  }
-  if (t <= kLnChunks) p.ticket[t] = 0u;
-}
 template <class E, int CHB, class Y = E, int RPI = DTA_LN_BWD_RPI>
 __global__ __launch_bounds__(256) void ln_bwd_rb_kernel(LnParams p) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -485,12 +434,12 @@ __global__ __launch_bounds__(256) void ln_bwd_rb_kernel(LnParams p) {
       }
     }
   }
-  if (p.partial && p.ticket) ln_bwd_fold(p, t);
 }
 
 // dw / db += the column sums of the per-block partials, in a fixed order: pass 1 sums
 // each of kLnChunks contiguous runs of blocks per column (many threads in flight),
 // pass 2 adds the kLnChunks run sums in order
+constexpr int kLnChunks = 32;
 __global__ __launch_bounds__(256) void ln_bwd_reduce1_kernel(const float* part, int nblk, int64_t C, float* part2) {
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;      // over 2 * C
   if (e >= 2 * C) return;
@@ -590,7 +539,7 @@ int ln_launch(const LnParams& p, bool bwd, hipStream_t st) {
         hipLaunchKernelGGL((ln_bwd_rb_kernel<E, (CH_ + 3) / 4>), dim3(bwd_grid), dim3(256), 0, st, p); \
       else                                                                             \
         hipLaunchKernelGGL((ln_bwd_kernel<E, CH_>), dim3(bwd_grid), dim3(256), 0, st, p); \
-      if (p.partial && !(p.ticket && DTA_LN_BWD_ROWBLOCK && CH_ <= 16 && (CH_ + 3) / 4 * 2048 >= p.C)) { \
+      if (p.partial) {                                                                 \
         float* part2 = p.partial + (int64_t)bwd_grid * 2 * p.C;                        \
         const unsigned g = (unsigned)((2 * p.C + 255) / 256);                          \
         hipLaunchKernelGGL(ln_bwd_reduce1_kernel, dim3(g, kLnChunks), dim3(256), 0, st, p.partial, bwd_grid, p.C, part2); \
@@ -616,7 +565,7 @@ int ln_launch_mixed(const LnParams& p, bool bwd, hipStream_t st) {
   if (ch <= CH_) {                                                                               \
     if (bwd) {                                                                                   \
       hipLaunchKernelGGL((ln_bwd_rb_kernel<float, (CH_ + 3) / 4, Y>), dim3(bwd_grid), dim3(256), 0, st, p); \
-      if (p.partial && !p.ticket) {                                                              \
+      if (p.partial) {                                                                           \
         float* part2 = p.partial + (int64_t)bwd_grid * 2 * p.C;                                  \
         const unsigned g = (unsigned)((2 * p.C + 255) / 256);                                    \
         hipLaunchKernelGGL(ln_bwd_reduce1_kernel, dim3(g, kLnChunks), dim3(256), 0, st, p.partial, bwd_grid, p.C, part2); \

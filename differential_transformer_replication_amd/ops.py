@@ -336,7 +336,6 @@ class _GroupLNScale(torch.autograd.Function):
         a = _lib.LnArgs(_lib.dtype_code(x2.dtype), x2.shape[0], C, eps, out_scale, x2.data_ptr(), C, None, 0,
                         w32.data_ptr(), None, mean.data_ptr(), rstd.data_ptr(), dy2.data_ptr(), C,
                         dx.data_ptr(), C, dw.data_ptr(), db.data_ptr(), part.data_ptr(), io)
-        a.ticket = _lib.ln_ticket(x2.device).data_ptr()     # the ordered reduce inside the kernel
         _lib.check(lib.dta_ln_bwd(a, _lib.stream_handle(x2.device)))
         if g is not None:
             hook = ctx.bound[0]["on_ready"]
@@ -402,8 +401,7 @@ class _AddLN(torch.autograd.Function):
         args = _lib.LnArgs(_lib.DTA_F32, xo.shape[0], C, eps, 1.0, xo.data_ptr(), C, None, 0, w32.data_ptr(), None,
                            mean.data_ptr(), rstd.data_ptr(), dy2.data_ptr(), C, dx.data_ptr(), C, dw.data_ptr(),
                            db.data_ptr(), part.data_ptr(), io, None, 0, None, 0,
-                           dres.data_ptr() if dres is not None else None, C, da.data_ptr(), C,
-                           _lib.ln_ticket(xo.device).data_ptr())
+                           dres.data_ptr() if dres is not None else None, C, da.data_ptr(), C)
         _lib.check(lib.dta_ln_bwd(args, _lib.stream_handle(xo.device)))
         da_out = da.view(xshape).to(adt)
         if g is not None:

@@ -200,11 +200,6 @@ typedef struct dta_ln_args {
   float* xo; int64_t xo_stride;          /* ... and writes x + res here (fp32, required with res) */
   const float* dres; int64_t dres_stride;  /* bwd: dx += dres (fp32 gradient of the residual branch) */
   void* dx16; int64_t dx16_stride;       /* bwd: dx also written in the y dtype */
-  uint32_t* ticket;                      /* ABI 7, bwd with partial, optional: 33 uint32 that are zero
-                                            on entry (and left zero): the ordered dw / db reduce of the
-                                            partials then runs inside the backward kernel (the last
-                                            workgroups sum them) instead of two more launches; same
-                                            bits either way.  Calls sharing a ticket must not overlap. */
 } dta_ln_args;
 
 int dta_ln_fwd(const dta_ln_args* a, void* stream);

@@ -39,45 +39,6 @@ def test_ln_backward_many_rows(dtype, rows, C):
     assert rel_err(bg.grad.cpu(), b64.grad) < tol
 
 
-@pytest.mark.parametrize("rows,C", [(32768, 2048), (4099, 1024), (9000, 384), (7, 64), (1, 8192)])
-def test_ln_backward_folded_reduce_bitwise(rows, C):
-    """ABI 7 dta_ln_args.ticket: the ordered dw / db reduce inside the backward kernel gives
-    bitwise the dw / db (and dx) of the two reduce launches it replaces, and leaves the
-    ticket counters zero for the next call (run twice)."""
-    from differential_transformer_replication_amd import _lib
-    lib = _lib.load()
-    g = torch.Generator(device=DEV).manual_seed(rows)
-    x = torch.randn(rows, C, device=DEV, generator=g).to(torch.bfloat16)
-    dy = torch.randn(rows, C, device=DEV, generator=g).to(torch.bfloat16)
-    w = 1 + 0.1 * torch.randn(C, device=DEV, generator=g)
-    mean = torch.empty(rows, device=DEV)
-    rstd = torch.empty(rows, device=DEV)
-    y = torch.empty_like(x)
-    st = _lib.stream_handle(torch.device(DEV))
-    fa = _lib.LnArgs(_lib.DTA_BF16, rows, C, 1e-5, 0.2, x.data_ptr(), C, y.data_ptr(), C, w.data_ptr(),
-                     torch.zeros(C, device=DEV).data_ptr(), mean.data_ptr(), rstd.data_ptr())
-    _lib.check(lib.dta_ln_fwd(fa, st))
-    ticket = torch.zeros(64, device=DEV, dtype=torch.int32)
-    outs = []
-    for use in (False, True, True):
-        dx = torch.empty_like(x)
-        dw = torch.full((C,), 0.25, device=DEV)
-        db = torch.full((C,), -0.5, device=DEV)
-        part = torch.full((lib.dta_ln_bwd_workspace_bytes(rows, C) // 4,), float("nan"), device=DEV)
-        ba = _lib.LnArgs(_lib.DTA_BF16, rows, C, 1e-5, 0.2, x.data_ptr(), C, None, 0, w.data_ptr(), None,
-                         mean.data_ptr(), rstd.data_ptr(), dy.data_ptr(), C, dx.data_ptr(), C, dw.data_ptr(),
-                         db.data_ptr(), part.data_ptr())
-        if use:
-            ba.ticket = ticket.data_ptr()
-        _lib.check(lib.dta_ln_bwd(ba, st))
-        torch.cuda.synchronize()
-        outs.append((dx, dw, db))
-        assert int(ticket.abs().sum()) == 0
-    for dx, dw, db in outs[1:]:
-        assert torch.equal(dx, outs[0][0])
-        assert torch.equal(dw, outs[0][1]) and torch.equal(db, outs[0][2])
-
-
 @pytest.mark.parametrize("autocast", [False, True])
 def test_block_layernorm_matches_torch(autocast):
     ops = _ops()

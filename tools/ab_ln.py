@@ -1,9 +1,7 @@
 """One-process A/B of libdiffattn builds on the LayerNorm kernels at the cfg2
 GroupLayerNorm shape (32768 rows x 2048, bf16): dta_ln_fwd and dta_ln_bwd (with the
 ordered dw/db reduce), HIP events, rounds interleaved; dx compared with the first build.
-    python tools/ab_ln.py base=lib/libdiffattn_x.so new=lib/libdiffattn.so [new_t=lib/libdiffattn.so]
-A build name ending in "_t" runs the backward with an ABI-7 ticket (the ordered dw/db reduce
-inside the kernel instead of two reduce launches)."""
+    python tools/ab_ln.py base=lib/libdiffattn_x.so new=lib/libdiffattn.so"""
 import ctypes
 import json
 import os
@@ -50,12 +48,10 @@ def main():
     ba = _lib.LnArgs(_lib.DTA_BF16, rows, C, 1e-5, 0.2, x.data_ptr(), C, None, 0, w.data_ptr(), None,
                      mean.data_ptr(), rstd.data_ptr(), dy.data_ptr(), C, dx.data_ptr(), C, dw.data_ptr(),
                      db.data_ptr(), part.data_ptr())
-    ticket = torch.zeros(64, device=dev, dtype=torch.int32)
     times = {n: {"fwd": [], "bwd": [], "rope": []} for n in libs}
     ref = None
     for rnd in range(6):
         for n, lib in libs.items():
-            ba.ticket = ticket.data_ptr() if n.endswith("_t") else None
             for kind, fn in (("fwd", lambda: lib.dta_ln_fwd(fa, stream)), ("bwd", lambda: lib.dta_ln_bwd(ba, stream)),
                              ("rope", lambda: lib.dta_rope(ra, stream))):
                 for _ in range(2):
