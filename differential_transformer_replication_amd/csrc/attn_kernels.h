@@ -1235,6 +1235,9 @@ struct DqCfg {
   static constexpr int bytes = (nQ + NS * nK + NS * nV) * (int)sizeof(E);
 };
 
+#ifndef DTA_DQ_PAIR3
+#define DTA_DQ_PAIR3 0
+#endif
 template <class E, int HS, int N, int DV = 2 * HS, bool NP = false>
 struct DqPick {
   static constexpr int LIM = 160 * 1024;
@@ -1243,12 +1246,17 @@ struct DqPick {
   static constexpr int QRH = (q8 && (N >= 2 || DTA_PAIR_N1) &&
                               DqCfg<E, HS, N, DV, 4, false, 1>::bytes <= 80 * 1024) ? 1 : 0;
   // (head size >= 64: the hs = 32, N = 3 paired plan spills)
-  static constexpr bool pair = !NP && QRH == 1 && q8 && HS >= 64 &&
-                               DqCfg<E, HS, N, DV, 4, false, QRH>::bytes <= 80 * 1024;
+  static constexpr bool pair64 = !NP && QRH == 1 && q8 && HS >= 64 &&
+                                 DqCfg<E, HS, N, DV, 4, false, QRH>::bytes <= 80 * 1024;
+  // A/B (DTA_DQ_PAIR3): N >= 3 at head size 64, where no 8-wave plan fits, in the paired
+  // layout with 32-key tiles (branch 0's Q in registers) instead of one wave per SIMD
+  static constexpr bool pair32 = DTA_DQ_PAIR3 && !NP && !pair64 && sizeof(E) == 2 && N >= 3 && HS == 64 &&
+                                 DqCfg<E, HS, N, DV, 4, false, 1, true>::bytes <= 80 * 1024;
+  static constexpr bool pair = pair64 || pair32;
   static constexpr int NW = pair ? 4 : (q8 ? 8 : (sizeof(E) == 2 ? 4 : 2));
   static constexpr bool QREG = pair ? false : !q8;
-  static constexpr int QH = pair ? QRH : 0;
-  static constexpr bool B32 = DqCfg<E, HS, N, DV, NW, QREG, QH>::bytes > LIM;   // 32-key tiles (fallback)
+  static constexpr int QH = pair ? 1 : 0;
+  static constexpr bool B32 = pair32 || DqCfg<E, HS, N, DV, NW, QREG, QH>::bytes > LIM;   // 32-key tiles
   static constexpr bool ok = DqCfg<E, HS, N, DV, NW, QREG, QH, B32>::bytes <= LIM;
 };
 
