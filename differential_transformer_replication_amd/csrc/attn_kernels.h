@@ -1235,8 +1235,13 @@ struct DqCfg {
   static constexpr int bytes = (nQ + NS * nK + NS * nV) * (int)sizeof(E);
 };
 
+// N = 3 at head size 64 (cfg3): no 8-wave plan fits, so the dQ plan was one wave per
+// SIMD (Q of all branches in registers, 160 AGPRs).  In the paired layout with 32-key
+// tiles (branch 0's Q in registers, branches 1-2 in LDS, 72 KB, 252 VGPRs, no spill) it is
+// faster: one-process A/B (profiles/r05g_ab_dq_pair3.json) cfg3 B=16 H=6 T=2048 dQ 0.414 ->
+// 0.379 ms, B=8 H=16 T=4096 1.683 -> 1.329 ms.  DTA_DQ_PAIR3 = 0 (A/B builds) keeps one wave.
 #ifndef DTA_DQ_PAIR3
-#define DTA_DQ_PAIR3 0
+#define DTA_DQ_PAIR3 1
 #endif
 template <class E, int HS, int N, int DV = 2 * HS, bool NP = false>
 struct DqPick {
@@ -1248,8 +1253,8 @@ struct DqPick {
   // (head size >= 64: the hs = 32, N = 3 paired plan spills)
   static constexpr bool pair64 = !NP && QRH == 1 && q8 && HS >= 64 &&
                                  DqCfg<E, HS, N, DV, 4, false, QRH>::bytes <= 80 * 1024;
-  // A/B (DTA_DQ_PAIR3): N >= 3 at head size 64, where no 8-wave plan fits, in the paired
-  // layout with 32-key tiles (branch 0's Q in registers) instead of one wave per SIMD
+  // N >= 3 at head size 64, where no 8-wave plan fits: the paired layout with 32-key
+  // tiles (branch 0's Q in registers) instead of one wave per SIMD (DTA_DQ_PAIR3)
   static constexpr bool pair32 = DTA_DQ_PAIR3 && !NP && !pair64 && sizeof(E) == 2 && N >= 3 && HS == 64 &&
                                  DqCfg<E, HS, N, DV, 4, false, 1, true>::bytes <= 80 * 1024;
   static constexpr bool pair = pair64 || pair32;
