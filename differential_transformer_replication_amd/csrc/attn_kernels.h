@@ -673,11 +673,14 @@ struct FwdChunk {
   static constexpr int DVC = DV <= cap ? DV : (cap >= 128 && DV % 128 == 0 ? 128 : (cap >= 64 ? 64 : 32));
 };
 
+#ifndef DTA_FWD_BN32
+#define DTA_FWD_BN32 0           // A/B: the paired forward plans with 32-key tiles
+#endif
 template <class E, int HS, int N, int DVC, int NW, bool QREG, int QRH = 0>
 struct FwdCfg {
   // QRH > 0 (paired plan): the first QRH branches' Q rows stay in registers
   static constexpr bool PAIR = NW == 4 && !QREG && sizeof(E) == 2 && N * DVC / 2 <= 128;
-  static constexpr int BN = (PAIR && QRH == 0) ? 32 : FwdTile<E>::BN;
+  static constexpr int BN = (PAIR && (QRH == 0 || DTA_FWD_BN32)) ? 32 : FwdTile<E>::BN;
   static constexpr int BM = NW * 32;
   static constexpr int HSP = img_cols(HS), DVP = img_cols(DVC);     // LDS image widths
   static constexpr int nQ = QREG ? 0 : (N - QRH) * BM * HSP;
@@ -1243,6 +1246,9 @@ struct DqCfg {
 #ifndef DTA_DQ_PAIR3
 #define DTA_DQ_PAIR3 1
 #endif
+#ifndef DTA_DQ_B32_N2
+#define DTA_DQ_B32_N2 0          // A/B: the paired N = 2 dQ plan with 32-key tiles
+#endif
 template <class E, int HS, int N, int DV = 2 * HS, bool NP = false>
 struct DqPick {
   static constexpr int LIM = 160 * 1024;
@@ -1261,7 +1267,8 @@ struct DqPick {
   static constexpr int NW = pair ? 4 : (q8 ? 8 : (sizeof(E) == 2 ? 4 : 2));
   static constexpr bool QREG = pair ? false : !q8;
   static constexpr int QH = pair ? 1 : 0;
-  static constexpr bool B32 = pair32 || DqCfg<E, HS, N, DV, NW, QREG, QH>::bytes > LIM;   // 32-key tiles
+  static constexpr bool B32 = pair32 || (DTA_DQ_B32_N2 && pair64 && N == 2) ||
+                              DqCfg<E, HS, N, DV, NW, QREG, QH>::bytes > LIM;   // 32-key tiles
   static constexpr bool ok = DqCfg<E, HS, N, DV, NW, QREG, QH, B32>::bytes <= LIM;
 };
 
