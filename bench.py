@@ -355,7 +355,7 @@ def configs_leg(args):
             raise RuntimeError(f"cfg3 n_terms={n} leg failed: {proc.stderr[-2000:]}")
         r = json.loads(proc.stdout.strip().splitlines()[-1])
         torch.cuda.empty_cache()
-        sec, flop, kernels = core_run(16, 6, 64, n, 2048, args.cfg_steps, 2)
+        sec, flop, kernels = core_run(16, 6, 64, n, 2048, args.cfg_steps, 5)   # warm after the training leg's idle host time
         out[f"cfg3_n{n}"] = {"train_tokens_per_s": r["value"], "train_ms_per_step": r["ms_per_step"],
                              "mfu": r.get("mfu"), "params": r["config"]["params"],
                              "core": {"shape": "B=16 H=6 hs=64 dv=128 T=2048 bf16 causal", "ms_per_step": round(
@@ -579,7 +579,7 @@ def main():
     ap.add_argument("--no-hbm", dest="hbm", action="store_false", help="kernel mode: skip the LN / RoPE timings")
     ap.add_argument("--no-configs", dest="configs", action="store_false",
                     help="kernel mode: skip the cfg3 / cfg5 legs (one GPU only)")
-    ap.add_argument("--cfg-steps", type=int, default=6, help="timed steps of each cfg3 / cfg5 leg")
+    ap.add_argument("--cfg-steps", type=int, default=10, help="timed steps of each cfg3 / cfg5 leg")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--traffic", type=float, default=None,
                     help="HBM bytes per dominant-kernel launch from rocprofv3 PMC (profiles/)")

@@ -87,10 +87,24 @@ def main():
                               _lib.tensor5(dk), _lib.tensor5(dvv), dcoef.data_ptr(), delta.data_ptr(), None,
                               _lib.BWD_PRE, None)
         ba.obr_dtype = fa.obr_dtype
-        state[name] = (lib, fa, ba, (o, obr, lse, dqkv, dcoef))
+        # as ops._DiffAttention.backward: fixed-order d(coef) partials, and the fp32 dV
+        # workspace when dK/dV runs in more than one branch group
+        lib.dta_attn_bwd_dcoef_partial_bytes.argtypes = [ctypes.c_int32] * 4
+        lib.dta_attn_bwd_dcoef_partial_bytes.restype = ctypes.c_size_t
+        dcp = torch.empty(lib.dta_attn_bwd_dcoef_partial_bytes(B, T, H, N) // 4, device=dev)
+        ba.dcoef_partial = dcp.data_ptr()
+        keep = [dcp]
+        if hasattr(lib, "dta_attn_bwd_dkdv_groups"):
+            lib.dta_attn_bwd_dkdv_groups.argtypes = [ctypes.c_int32] * 5
+            lib.dta_attn_bwd_dkdv_groups.restype = ctypes.c_int
+            if lib.dta_attn_bwd_dkdv_groups(0, hs, N, dv, 0) > 1:
+                dv32 = torch.empty(B, T, H, dv, device=dev)
+                ba.dv_f32 = dv32.data_ptr()
+                keep.append(dv32)
+        state[name] = (lib, fa, ba, (o, obr, lse, dqkv, dcoef), keep)
 
     def run(name, which):
-        lib, fa, ba, _ = state[name]
+        lib, fa, ba, _, _ = state[name]
         if which == "fwd":
             rc = lib.dta_attn_fwd(fa, stream)
         else:
