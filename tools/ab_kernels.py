@@ -36,7 +36,7 @@ def load(path):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("builds", nargs="+", help="name=path (path relative to the package dir)")
+    ap.add_argument("builds", nargs="+", help="name=path[@qcap,kcap] (path relative to the package dir)")
     ap.add_argument("--shape", default="8,16,64,2,4096")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=10)
@@ -47,8 +47,12 @@ def main():
     dv = args.dv or 2 * hs
     dev = torch.device("cuda", 0)
     builds = []
+    caps = {}
     for b in args.builds:
         name, path = b.split("=", 1)
+        if "@" in path:                   # name=path@qcap,kcap: ABI 7 backward branch-group caps
+            path, c = path.split("@", 1)
+            caps[name] = tuple(int(x) for x in c.split(","))
         builds.append((name, load(path if os.path.isabs(path) else os.path.join(LIBDIR, path))))
     g = torch.Generator(device=dev).manual_seed(0)
     W = 2 * H * N * hs + H * dv
@@ -87,6 +91,7 @@ def main():
                               _lib.tensor5(dk), _lib.tensor5(dvv), dcoef.data_ptr(), delta.data_ptr(), None,
                               _lib.BWD_PRE, None)
         ba.obr_dtype = fa.obr_dtype
+        ba.group_max_dq, ba.group_max_dkdv = caps.get(name, (0, 0))
         # as ops._DiffAttention.backward: fixed-order d(coef) partials, and the fp32 dV
         # workspace when dK/dV runs in more than one branch group
         lib.dta_attn_bwd_dcoef_partial_bytes.argtypes = [ctypes.c_int32] * 4
@@ -97,7 +102,7 @@ def main():
         if hasattr(lib, "dta_attn_bwd_dkdv_groups"):
             lib.dta_attn_bwd_dkdv_groups.argtypes = [ctypes.c_int32] * 5
             lib.dta_attn_bwd_dkdv_groups.restype = ctypes.c_int
-            if lib.dta_attn_bwd_dkdv_groups(0, hs, N, dv, 0) > 1:
+            if lib.dta_attn_bwd_dkdv_groups(0, hs, N, dv, ba.group_max_dkdv) > 1:
                 dv32 = torch.empty(B, T, H, dv, device=dev)
                 ba.dv_f32 = dv32.data_ptr()
                 keep.append(dv32)
