@@ -673,6 +673,9 @@ struct FwdChunk {
   static constexpr int DVC = DV <= cap ? DV : (cap >= 128 && DV % 128 == 0 ? 128 : (cap >= 64 ? 64 : 32));
 };
 
+#ifndef DTA_EPI_SKIP
+#define DTA_EPI_SKIP 0           // measurement only (wrong results): 1 skips the attention kernels' output stores, 2 the forward's O_i stores
+#endif
 #ifndef DTA_FWD_BN32
 #define DTA_FWD_BN32 0           // A/B: the paired forward plans with 32-key tiles
 #endif
@@ -728,6 +731,58 @@ struct FwdPick {
   static constexpr bool ok = FwdCfg<E, HS, N, DVC, NW, QREG, QH>::bytes <= LIM;
 };
 
+// Epilogue stores through an LDS bounce.  In the 32x32 accumulator layout a lane holds row
+// (lane & 31), columns d*32 + 8g + 4hf + 0..3, so a direct store instruction writes 32 rows
+// x 16 B per half-wave (32 cache lines); bounced through a per-wave LDS region (32 rows x 64
+// fp32 = 8 KB, 16-byte chunks XOR-swizzled by row) every store instruction writes whole
+// 256-byte row segments: 4 rows of 64 fp32, or 8 rows of 64 16-bit values.  A wave's own
+// LDS accesses complete in order, so no wait sits between the write and the read.
+// val(d, g) returns the lane's 4 values of column block d, group g; rows >= nrows are not
+// stored.  dst: row 0, column 0 of the wave's tile; ld: row stride in OutT elements.
+#ifndef DTA_FWD_BOUNCE
+#define DTA_FWD_BOUNCE 1
+#endif
+#ifndef DTA_BWD_BOUNCE
+#define DTA_BWD_BOUNCE 1
+#endif
+template <class OutT, int NDB, class Val>
+__device__ __forceinline__ void bounce_store(float* reg, int lane, Val&& val, OutT* dst, int64_t ld, int nrows) {
+  const int r = lane & 31, hf = lane >> 5;
+#pragma unroll
+  for (int h = 0; h < NDB / 2; ++h) {
+#pragma unroll
+    for (int dd = 0; dd < 2; ++dd)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int c = dd * 8 + 2 * g + hf;
+        *reinterpret_cast<f32x4*>(reg + r * 64 + ((c ^ (r & 15)) << 2)) = val(2 * h + dd, g);
+      }
+    if constexpr (sizeof(OutT) == 4) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int rr = k * 4 + (lane >> 4), c = lane & 15;
+        const f32x4 v = *reinterpret_cast<const f32x4*>(reg + rr * 64 + ((c ^ (rr & 15)) << 2));
+        if (rr < nrows) *reinterpret_cast<f32x4*>(dst + rr * ld + h * 64 + c * 4) = v;
+      }
+    } else {
+      typedef OutT v8 __attribute__((ext_vector_type(8)));
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int rr = k * 8 + (lane >> 3), c = (lane & 7) * 2;
+        const f32x4 a = *reinterpret_cast<const f32x4*>(reg + rr * 64 + ((c ^ (rr & 15)) << 2));
+        const f32x4 bq = *reinterpret_cast<const f32x4*>(reg + rr * 64 + (((c + 1) ^ (rr & 15)) << 2));
+        const v8 v = {(OutT)a[0], (OutT)a[1], (OutT)a[2], (OutT)a[3], (OutT)bq[0], (OutT)bq[1], (OutT)bq[2], (OutT)bq[3]};
+        if (rr < nrows) *reinterpret_cast<v8*>(dst + rr * ld + h * 64 + c * 4) = v;
+      }
+    }
+  }
+}
+__device__ __forceinline__ bool t5_aligned16(const T5& t, int esize) {
+  const int64_t m = 16 / esize;
+  return (reinterpret_cast<uintptr_t>(t.p) & 15) == 0 && t.sb % m == 0 && t.st % m == 0 && t.sh % m == 0 &&
+         t.si % m == 0;
+}
+
 // SEQ (N = 1 paired plans only): the workgroup runs p.bseq branches one after another over
 // the same query block -- each branch's key loop, O_i and LSE_i as a branch-split
 // workgroup would -- and keeps O = sum_i c_i O_i in registers across them, so the
@@ -777,6 +832,11 @@ void attn_fwd_kernel(FwdParams p) {
   int qrow = qw0 + c32;
 
   static_assert(!SEQ || (N == 1 && QRH == 1 && DVC == 2 * HS && !DROP), "SEQ: N = 1 paired plans, whole dv");
+  // the bounced epilogue (see bounce_store): 16-bit plans with whole 64-column passes, a
+  // ring that holds a region per wave, fp32 O_i and 16-byte aligned outputs
+  constexpr bool BNC = DTA_FWD_BOUNCE && sizeof(E) == 2 && NDB % 2 == 0 &&
+                       NS * (CF::nK + CF::nV) * (int)sizeof(E) >= NW * 8192;
+  const bool bnc = BNC && !p.ob16 && t5_aligned16(p.obr, 4) && (nsp > 1 || t5_aligned16(p.o, sizeof(E)));
   const int nseq = SEQ ? p.bseq : 1;
   const E* gq = reinterpret_cast<const E*>(p.q.p) + b * p.q.sb + hh * p.q.sh + br * p.q.si;
   const E* gk = reinterpret_cast<const E*>(p.k.p) + b * p.k.sb + hh * p.k.sh + br * p.k.si;
@@ -1170,7 +1230,53 @@ void attn_fwd_kernel(FwdParams p) {
   st.lap<5>();
   st.flush(p.stamps, lin * NW + wave, lane);
 
-  if (!SEQ && (!wave_live || qrow >= T)) return;
+  if (!SEQ && !wave_live) return;
+  if (DTA_EPI_SKIP == 1 && p.T != -7) return;
+  if (bnc) {
+    if (wave_live) {
+      float inv[N];
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        const float lt = wave_sum_halves(l[i]);
+        inv[i] = 1.f / lt;
+        if (dc0 == 0 && hf == 0 && qrow < T)
+          p.lse[(((int64_t)(brs + i) * p.B + b) * p.H + hh) * T + qrow] = -(m[i] + __builtin_log2f(lt));   // stored negated
+      }
+      float* reg = reinterpret_cast<float*>(Kb) + wave * 2048;    // the ring is idle
+      const int nrows = min(32, T - qw0);
+      float* gob0 = reinterpret_cast<float*>(p.obr.p) + b * p.obr.sb + (int64_t)qw0 * p.obr.st + hh * p.obr.sh +
+                    brs * p.obr.si + dc0;
+#pragma unroll
+      for (int i = 0; i < N; ++i)
+        bounce_store<float, NDB>(reg, lane, [&](int d, int g) {
+          return f32x4{acc[i][d][4 * g] * inv[i], acc[i][d][4 * g + 1] * inv[i], acc[i][d][4 * g + 2] * inv[i],
+                       acc[i][d][4 * g + 3] * inv[i]};
+        }, gob0 + i * p.obr.si, p.obr.st, nrows);
+      auto osum = [&](int d, int g) {
+        f32x4 o = f32x4{};
+#pragma unroll
+        for (int i = 0; i < N; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] = fmaf(coef[i], acc[i][d][4 * g + j] * inv[i], o[j]);
+        return o;
+      };
+      if constexpr (SEQ) {
+#pragma unroll
+        for (int d = 0; d < NDB; ++d)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const f32x4 o = osum(d, g);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) oacc[d < NDBS ? d : 0][4 * g + j] += o[j];
+          }
+      } else if (nsp == 1) {
+        E* go0 = reinterpret_cast<E*>(p.o.p) + b * p.o.sb + (int64_t)qw0 * p.o.st + hh * p.o.sh + dc0;
+        bounce_store<E, NDB>(reg, lane, osum, go0, p.o.st, nrows);
+      }
+    }
+    if constexpr (SEQ) lds_barrier();       // the next branch's ring prologue overwrites the regions
+  } else {
+  if (!SEQ && qrow >= T) return;
   if (wave_live && qrow < T) {      // (SEQ: every lane stays for the next branch's barriers)
   float inv[N];
 #pragma unroll
@@ -1194,7 +1300,7 @@ void attn_fwd_kernel(FwdParams p) {
       for (int i = 0; i < N; ++i) {
         const float a0 = acc[i][d][4 * g + 0] * inv[i], a1 = acc[i][d][4 * g + 1] * inv[i];
         const float a2 = acc[i][d][4 * g + 2] * inv[i], a3 = acc[i][d][4 * g + 3] * inv[i];
-        store_ob4(p.obr.p, gob + i * p.obr.si + e, p.ob16, a0, a1, a2, a3);
+        if (DTA_EPI_SKIP != 2 || p.T == -7) store_ob4(p.obr.p, gob + i * p.obr.si + e, p.ob16, a0, a1, a2, a3);
         o0 = fmaf(coef[i], a0, o0); o1 = fmaf(coef[i], a1, o1);
         o2 = fmaf(coef[i], a2, o2); o3 = fmaf(coef[i], a3, o3);
       }
@@ -1206,9 +1312,18 @@ void attn_fwd_kernel(FwdParams p) {
       }
     }
   }
+  }   // bnc
   }   // branches (SEQ)
   if constexpr (SEQ) {
-    if (qw0 >= T || qrow >= T) return;
+    if (qw0 >= T) return;
+    if (bnc) {
+      E* go0 = reinterpret_cast<E*>(p.o.p) + b * p.o.sb + (int64_t)qw0 * p.o.st + hh * p.o.sh + dc0;
+      bounce_store<E, NDBS>(reinterpret_cast<float*>(Kb) + wave * 2048, lane, [&](int d, int g) {
+        return f32x4{oacc[d][4 * g], oacc[d][4 * g + 1], oacc[d][4 * g + 2], oacc[d][4 * g + 3]};
+      }, go0, p.o.st, min(32, T - qw0));
+      return;
+    }
+    if (qrow >= T) return;
     E* go = reinterpret_cast<E*>(p.o.p) + b * p.o.sb + (int64_t)qrow * p.o.st + hh * p.o.sh + dc0;
 #pragma unroll
     for (int d = 0; d < NDBS; ++d)
@@ -1633,6 +1748,34 @@ void attn_dq_kernel(BwdParams p) {
   for (int kt = 0; kt < nfull; ++kt) step(kt, std::false_type{});
   for (int kt = nfull; kt < ntiles; ++kt) step(kt, std::true_type{});
 
+  if (qw0 >= T) return;
+  if (DTA_EPI_SKIP == 1 && p.T != -7) return;
+  // bounced epilogue (see bounce_store; the ring is idle): whole-row store instructions
+  constexpr bool BNC = DTA_BWD_BOUNCE && sizeof(E) == 2 && NHB % 2 == 0 && CF::bytes >= NW * 8192;
+  if constexpr (BNC) {
+    if (OUTF32 || t5_aligned16(p.dq, sizeof(E))) {
+      float* reg = reinterpret_cast<float*>(smem) + wave * 2048;
+      const int nrows = min(32, T - qw0);
+      const int rrow = min(qrow, T - 1);       // RoPE table row (rows past T are not stored)
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        const float sc = SEED ? p.scale * coef[i] : p.scale;
+        auto val = [&](int d, int g) {
+          float a0 = dq[i][d][4 * g] * sc, a1 = dq[i][d][4 * g + 1] * sc;
+          float a2 = dq[i][d][4 * g + 2] * sc, a3 = dq[i][d][4 * g + 3] * sc;
+          if (p.rope) rope_inv4(p.rope, rrow, HS, d * 32 + 8 * g + 4 * hf, a0, a1, a2, a3);
+          return f32x4{a0, a1, a2, a3};
+        };
+        if constexpr (OUTF32)
+          bounce_store<float, NHB>(reg, lane, val, p.dq32 + ((((int64_t)b * T + qw0) * p.H + hh) * p.cst + i) * HS,
+                                   (int64_t)p.H * p.cst * HS, nrows);
+        else
+          bounce_store<E, NHB>(reg, lane, val, reinterpret_cast<E*>(p.dq.p) + b * p.dq.sb + (int64_t)qw0 * p.dq.st +
+                                                   hh * p.dq.sh + i * p.dq.si, p.dq.st, nrows);
+      }
+      return;
+    }
+  }
   if (!rowok) return;
 #pragma unroll
   for (int i = 0; i < N; ++i)
@@ -2145,7 +2288,66 @@ void attn_dkdv_kernel(BwdParams p) {
   for (int t = ttail; t < ntiles; ++t) step(t, std::true_type{});
   st.flush(p.stamps, lin * NW + wave, lane);
 
-  if (!wave_keys || krow >= T) return;
+  if (!wave_keys) return;
+  if (DTA_EPI_SKIP == 1 && p.T != -7) return;
+  // bounced epilogue (see bounce_store; the ring and the K_i rows are idle): dK, and dV
+  // unless it adds to an earlier branch group's partial
+  constexpr bool BNC = DTA_BWD_BOUNCE && sizeof(E) == 2 && (!DK || NHB % 2 == 0) && (!DVV || NVB % 2 == 0) &&
+                       CF::bytes >= NW * 8192;
+  if constexpr (BNC) {
+    float* g32 = p.dv32 ? p.dv32 + (((int64_t)b * p.T + kw0) * p.H + hh) * p.DV : nullptr;
+    const bool to32 = g32 != nullptr && !p.dv_last;
+    if ((!DK || t5_aligned16(p.dk, sizeof(E))) && (!DVV || p.dv_acc || to32 || t5_aligned16(p.dv, sizeof(E)))) {
+      float* reg = reinterpret_cast<float*>(smem) + wave * 2048;
+      const int nrows = min(32, T - kw0);
+      const int rrow = min(krow, T - 1);       // RoPE table row (rows past T are not stored)
+      if constexpr (DK) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+          const float sc = p.scale * coef[i];      // dS_i was accumulated without its c_i
+          bounce_store<E, NHB>(reg, lane, [&](int d, int g) {
+            float a0 = dk[i][d][4 * g] * sc, a1 = dk[i][d][4 * g + 1] * sc;
+            float a2 = dk[i][d][4 * g + 2] * sc, a3 = dk[i][d][4 * g + 3] * sc;
+            if (p.rope) rope_inv4(p.rope, rrow, HS, d * 32 + 8 * g + 4 * hf, a0, a1, a2, a3);
+            return f32x4{a0, a1, a2, a3};
+          }, reinterpret_cast<E*>(p.dk.p) + b * p.dk.sb + (int64_t)kw0 * p.dk.st + hh * p.dk.sh + i * p.dk.si,
+             p.dk.st, nrows);
+        }
+      }
+      if constexpr (DVV) {
+        if (!p.dv_acc) {
+          auto val = [&](int d, int g) { return f32x4{dv[d][4 * g], dv[d][4 * g + 1], dv[d][4 * g + 2], dv[d][4 * g + 3]}; };
+          if (to32) bounce_store<float, NVB>(reg, lane, val, g32, (int64_t)p.H * p.DV, nrows);
+          else bounce_store<E, NVB>(reg, lane, val, reinterpret_cast<E*>(p.dv.p) + b * p.dv.sb + (int64_t)kw0 * p.dv.st +
+                                                       hh * p.dv.sh, p.dv.st, nrows);
+          return;
+        }
+      } else {
+        return;
+      }
+      // dV of a later branch group: the per-lane read-add-store below, after the bounced dK
+      if (krow >= T) return;
+      float* g32r = p.dv32 ? p.dv32 + (((int64_t)b * p.T + krow) * p.H + hh) * p.DV : nullptr;
+      E* gdv = reinterpret_cast<E*>(p.dv.p) + b * p.dv.sb + (int64_t)krow * p.dv.st + hh * p.dv.sh;
+#pragma unroll
+      for (int d = 0; d < (DVV ? NVB : 1); ++d)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int e = d * 32 + 8 * g + 4 * hf;
+          float a0 = dv[d][4 * g], a1 = dv[d][4 * g + 1], a2 = dv[d][4 * g + 2], a3 = dv[d][4 * g + 3];
+          if (g32r) {
+            const f32x4 v = *reinterpret_cast<const f32x4*>(g32r + e);
+            a0 += v[0]; a1 += v[1]; a2 += v[2]; a3 += v[3];
+          } else {
+            a0 += (float)gdv[e]; a1 += (float)gdv[e + 1]; a2 += (float)gdv[e + 2]; a3 += (float)gdv[e + 3];
+          }
+          if (to32) store4<float>(g32r + e, a0, a1, a2, a3);
+          else store4<E>(gdv + e, a0, a1, a2, a3);
+        }
+      return;
+    }
+  }
+  if (krow >= T) return;
   if constexpr (DK) {
     E* gdk = reinterpret_cast<E*>(p.dk.p) + b * p.dk.sb + (int64_t)krow * p.dk.st + hh * p.dk.sh;
 #pragma unroll
