@@ -1358,6 +1358,9 @@ struct DqCfg {
 // tiles (branch 0's Q in registers, branches 1-2 in LDS, 72 KB, 252 VGPRs, no spill) it is
 // faster: one-process A/B (profiles/r05g_ab_dq_pair3.json) cfg3 B=16 H=6 T=2048 dQ 0.414 ->
 // 0.379 ms, B=8 H=16 T=4096 1.683 -> 1.329 ms.  DTA_DQ_PAIR3 = 0 (A/B builds) keeps one wave.
+#ifndef DTA_DQ_EXPG
+#define DTA_DQ_EXPG 4            // exps per group ahead of their products in the dQ softmax (r05u: 1 -> 4, cfg2 dQ 0.888 -> 0.867 ms)
+#endif
 #ifndef DTA_DQ_PAIR3
 #define DTA_DQ_PAIR3 1
 #endif
@@ -1682,14 +1685,25 @@ void attn_dq_kernel(BwdParams p) {
           if constexpr (SEED) {
             // sa = S'_i (seeded with -LSE_i), dp = dP - delta_0: dS_i / c_i
             const float dd = ddel[i];
+            // DTA_DQ_EXPG exps issued before their products: a product right behind its
+            // exp waits a state on the transcendental result (s_nop)
 #pragma unroll
             for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
-              for (int r = 0; r < 16; ++r) {
-                float arg = sa[kb][r];
-                if constexpr (MASK) arg = (kb * 32 + (r & 3) + 8 * (r >> 2) > lim) ? -INFINITY : arg;
-                const float pr = exp2_fast(arg);
-                sa[kb][r] = i == 0 ? pr * dp[kb][r] : pr * (dp[kb][r] + dd);
+              for (int r0 = 0; r0 < 16; r0 += DTA_DQ_EXPG) {
+                float pr[DTA_DQ_EXPG];
+#pragma unroll
+                for (int u = 0; u < DTA_DQ_EXPG; ++u) {
+                  const int r = r0 + u;
+                  float arg = sa[kb][r];
+                  if constexpr (MASK) arg = (kb * 32 + (r & 3) + 8 * (r >> 2) > lim) ? -INFINITY : arg;
+                  pr[u] = exp2_fast(arg);
+                }
+#pragma unroll
+                for (int u = 0; u < DTA_DQ_EXPG; ++u) {
+                  const int r = r0 + u;
+                  sa[kb][r] = i == 0 ? pr[u] * dp[kb][r] : pr[u] * (dp[kb][r] + dd);
+                }
               }
           } else {
           uint32_t dkey = 0;
