@@ -98,6 +98,20 @@ def test_native_hs128_n3_sampled_rows(dtype):
                    dtype=dtype, seed=71)
 
 
+# ABI 6 obr_dtype = fp16 (ops: DTA_OBR_F16=1, 16-bit activations): O_i stored as fp16 for the
+# backward's delta_i.  The forward's epilogue then keeps its per-lane stores (the LDS bounce
+# takes fp32 O_i only), so this also covers that path; parity against fp64 at the usual bar.
+OBR16_CASES = [(2, 2, 64, 129, False), (2, 3, 64, 65, True), (1, 2, 128, 130, False), (1, 4, 32, 97, True)]
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("H,N,hs,T,rope", OBR16_CASES)
+def test_core_fp16_branch_outputs(dtype, H, N, hs, T, rope, monkeypatch):
+    monkeypatch.setenv("DTA_OBR_F16", "1")
+    assert _ops()._obr_dtype(dtype) == torch.float16
+    _core_case(dtype, H, N, hs, T, rope)
+
+
 def _core_case(dtype, H, N, hs, T, rope):
     ops = _ops()
     from differential_transformer_replication_amd import _lib
