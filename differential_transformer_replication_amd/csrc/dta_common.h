@@ -73,17 +73,25 @@ __device__ __forceinline__ int xcd_remap(int id, int n) {
 #ifndef DTA_LPT_GROUP
 #define DTA_LPT_GROUP 4
 #endif
+// Between 8 and 16 pairs per XCD the walk takes two equal groups instead of groups of
+// DTA_LPT_GROUP (cfg3's 12 pairs: 4 + 4 + 4 -> 6 + 6; one-process A/B profiles/r05zc_ab_lpt_groups.json:
+// cfg3 N = 3 fwd+dq+dkdv 1.099 -> 1.060 ms, N = 4 1.381 -> 1.344; cfg2's 16 pairs keep groups of
+// 4, its 2 x 8 measured equal).
+#ifndef DTA_LPT_HALVES
+#define DTA_LPT_HALVES 1
+#endif
 __device__ __forceinline__ void lpt_order(int& r, int& y, int& z, int& id) {
   id = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
   const int nyz = gridDim.y * gridDim.z;
   if (DTA_LPT && DTA_LPT_GROUP > 0 && nyz % 8 == 0) {
     const int xcd = id & 7, s = id >> 3;            // s-th block this XCD receives
     const int per = nyz >> 3, R = gridDim.x;        // pairs per XCD, work ranks
-    const int g = s / (R * DTA_LPT_GROUP);
-    const int gsz = min(DTA_LPT_GROUP, per - g * DTA_LPT_GROUP);
-    const int t = s - g * R * DTA_LPT_GROUP;
+    const int G = (DTA_LPT_HALVES && per > 8 && per < 16) ? (per + 1) / 2 : DTA_LPT_GROUP;
+    const int g = s / (R * G);
+    const int gsz = min(G, per - g * G);
+    const int t = s - g * R * G;
     r = t / gsz;
-    const int pair = xcd + 8 * (g * DTA_LPT_GROUP + t % gsz);
+    const int pair = xcd + 8 * (g * G + t % gsz);
     y = pair % gridDim.y;
     z = pair / gridDim.y;
     return;
