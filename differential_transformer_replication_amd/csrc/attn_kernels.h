@@ -45,21 +45,26 @@ namespace dta {
 // 7 'In-kernel stamps'): per-wave sums of the cycles between named points of the
 // tile loop, written once per wave to FwdParams/BwdParams::stamps.  The stamp's own
 // lgkmcnt(0) serialises LDS reads, so a stamped build is read for its SHARES only.
+template <int NSEG_ = 8>
 struct Stamps {
-  static constexpr int NSEG = 8;
-  unsigned long long t = 0, s[NSEG] = {};
-  __device__ __forceinline__ static unsigned long long now() {
+  // 32-bit sums (a wave's segment totals stay far below 2^32 cycles), and fewer segments
+  // where SGPRs are short: 8 64-bit sums cost the dK/dV plan enough SGPRs to spill its DMA
+  // offsets to scratch, which then serialised every LDS-DMA issue behind a scratch reload
+  // and inflated its 'dma_issue' share (round 6)
+  static constexpr int NSEG = NSEG_;
+  unsigned t = 0, s[NSEG] = {};
+  __device__ __forceinline__ static unsigned now() {
     unsigned long long v;
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : : "memory");
     __builtin_amdgcn_sched_barrier(0);
-    return v;
+    return (unsigned)v;
   }
   __device__ __forceinline__ void start() { if constexpr (DTA_STAMPS) t = now(); }
   template <int J>
   __device__ __forceinline__ void lap() {
     if constexpr (DTA_STAMPS) {
-      const unsigned long long n = now();
+      const unsigned n = now();
       s[J] += n - t;
       t = n;
     }
@@ -68,7 +73,7 @@ struct Stamps {
     if constexpr (DTA_STAMPS) {
       if (out && lane == 0)
 #pragma unroll
-        for (int j = 0; j < NSEG; ++j) out[(int64_t)wave_id * NSEG + j] = s[j];
+        for (int j = 0; j < 8; ++j) out[(int64_t)wave_id * 8 + j] = j < NSEG ? s[j] : 0;
     }
   }
 };
@@ -757,6 +762,10 @@ __device__ __forceinline__ void bounce_store(float* reg, int lane, Val&& val, Ou
         const int c = dd * 8 + 2 * g + hf;
         *reinterpret_cast<f32x4*>(reg + r * 64 + ((c ^ (r & 15)) << 2)) = val(2 * h + dd, g);
       }
+    // the reads below take values other lanes wrote, and the next h rewrites the region:
+    // pin the write -> read -> write order (a scheduling barrier only, no instruction; a
+    // wave's LDS operations then complete in issue order)
+    __builtin_amdgcn_wave_barrier();
     if constexpr (sizeof(OutT) == 4) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
@@ -775,6 +784,7 @@ __device__ __forceinline__ void bounce_store(float* reg, int lane, Val&& val, Ou
         if (rr < nrows) *reinterpret_cast<v8*>(dst + rr * ld + h * 64 + c * 4) = v;
       }
     }
+    __builtin_amdgcn_wave_barrier();
   }
 }
 __device__ __forceinline__ bool t5_aligned16(const T5& t, int esize) {
@@ -1152,7 +1162,7 @@ void attn_fwd_kernel(FwdParams p) {
   // two loops over straight-line bodies: tiles strictly below the block's first
   // query row and inside T need no mask; the block's diagonal / tail tiles do
   // (one loop body with both variants behind a branch spills)
-  Stamps st;
+  Stamps<> st;
   auto step = [&](int kt, auto MASKED, auto FASTT) {
     // keep lane-derived addresses loop-variant: recomputed per tile instead of
     // hoisted into (spilled) registers across the whole loop
@@ -1364,6 +1374,9 @@ struct DqCfg {
 #ifndef DTA_DQ_PAIR3
 #define DTA_DQ_PAIR3 1
 #endif
+#ifndef DTA_DQ_EARLY_RING
+#define DTA_DQ_EARLY_RING 0      // A/B: the K/V ring's first stages issued before the delta_i prologue
+#endif
 #ifndef DTA_DQ_B32_N2
 #define DTA_DQ_B32_N2 0          // A/B: the paired N = 2 dQ plan with 32-key tiles
 #endif
@@ -1459,6 +1472,12 @@ void attn_dq_kernel(BwdParams p) {
   // plans: up to 532 B/lane) read LDS only through compiler-tracked loads: no asm read
   // whose destination the allocator could spill before it lands (see tr_load)
   constexpr bool SPILLS = sizeof(E) == 2 && (DROP || (HS >= 128 && N >= 3));
+  // DTA_DQ_EARLY_RING: the ring's first stages are issued before the per-row loads and the
+  // delta_i reduction below, so their DMA overlaps the O_i reads instead of following them
+  constexpr bool EARLY = DTA_DQ_EARLY_RING && SRD;
+  if constexpr (EARLY)
+    for (int j = 0; j < NS - 1; ++j)
+      if (j < ntiles) stage_kv(j, j);
   // ---- per-row operands in registers: Q_i and dO rows (B operands), LSE, delta
   frag qf[NQR > 0 ? NQR : 1][NQR > 0 ? NSQ : 1], df[NSV];
   float coef[N], lse[N], del[N];
@@ -1524,8 +1543,10 @@ void attn_dq_kernel(BwdParams p) {
   }
   const int tile_pieces = SRD ? KR::pieces(wave)
                               : N * stage_pieces<E, HSP, BN, HS, NW>(wave) + stage_pieces<E, DVP, BN, DV, NW>(wave);
-  for (int j = 0; j < NS - 1; ++j)
-    if (j < ntiles) stage_kv(j, j);
+  if constexpr (!EARLY)
+    for (int j = 0; j < NS - 1; ++j)
+      if (j < ntiles) stage_kv(j, j);
+  // (EARLY: younger loads and stores follow the ring's pieces, so this waits for at least them)
   wait_vm(tile_pieces * max(0, min(NS - 1, ntiles) - 1));
   lds_barrier();
   // SEED: the LDS-resident Q_i rows pre-scaled by sl2 once; the seed fragments
@@ -1565,6 +1586,7 @@ void attn_dq_kernel(BwdParams p) {
     LrV = row_lane<VI::ROWB>(lane); LrK = row_lane<KI::ROWB>(lane); LrQ = row_lane<QI::ROWB>(lane);
     LtK = tr_lane<KI::ROWB>(lane);
   }
+  Stamps<5> st;   // diagnostic builds only (DTA_STAMPS): dma_issue | dP | S,dS,dQ of every branch | wait_vm | barrier
   auto step = [&](int kt, auto MASKED) {
     constexpr bool MASK = decltype(MASKED)::value;
     // keep lane-derived addresses loop-variant: recomputed per tile instead of
@@ -1582,6 +1604,7 @@ void attn_dq_kernel(BwdParams p) {
     qrow = qw0 + c32;
     const int buf = kt % NS;
     if (kt + NS - 1 < ntiles) stage_kv(kt + NS - 1, (kt + NS - 1) % NS);
+    st.lap<0>();
     const int k0 = kt * BN;
     if (wave_live && k0 <= qw0 + 31) {
       const E* Kc = Kb + buf * CF::nK;
@@ -1632,6 +1655,7 @@ void attn_dq_kernel(BwdParams p) {
             for (int s = 0; s < NSV; ++s) dp[kb] = O::mma(VI::row(Vc, kb * 32 + c32, s, hf), df[s], dp[kb]);
           }
         }
+        st.lap<1>();
         sfor<N>([&](auto I_) {
           constexpr int i = decltype(I_)::value;
           const E* Ki = Kc + i * BN * HSP;
@@ -1755,12 +1779,17 @@ void attn_dq_kernel(BwdParams p) {
         });
       }
     }
+    st.lap<2>();
     wait_vm(tile_pieces * max(0, min(NS - 2, ntiles - 2 - kt)));
+    st.lap<3>();
     lds_barrier();
+    st.lap<4>();
   };
+  st.start();
   const int nfull = min(ntiles, min((q0 + 1) / BN, T / BN));
   for (int kt = 0; kt < nfull; ++kt) step(kt, std::false_type{});
   for (int kt = nfull; kt < ntiles; ++kt) step(kt, std::true_type{});
+  st.flush(p.stamps, lin * NW + wave, lane);
 
   if (qw0 >= T) return;
   if (DTA_EPI_SKIP == 1 && p.T != -7) return;
@@ -2074,7 +2103,9 @@ void attn_dkdv_kernel(BwdParams p) {
   // masked diagonal tiles, unmasked interior, masked ragged tail tile; each loop
   // is one straight-line body (both variants behind a branch spill).  Lanes with
   // key >= T only pollute their own (never stored) dK/dV columns.
-  Stamps st;
+  // diagnostic builds only (DTA_STAMPS): dma_issue | dP, S, dS, dK, dV | wait_vm | barrier (four sums:
+  // more SGPRs spill this plan's DMA offsets)
+  Stamps<4> st;
   // per-lane LDS read bases, one register each across the loop: every read of a step
   // is then one v_xad (base ^ k-step) + stage
   int LrD = 0, LrQ = 0, LrK = 0, LtQ = 0, LtD = 0;
@@ -2155,7 +2186,6 @@ void attn_dkdv_kernel(BwdParams p) {
           for (int s = 0; s < NSV; ++s) dpa = O::mma(DI::row(Dc, c32, s, hf), vf[s], dpa);
         }
       }
-      st.lap<1>();
       f32x16 pc = f32x16{};
       // rows q0 + rowof(r) > lim are masked: query < key, or past the end
       const int lim_lo = krow - q0 - 4 * hf;          // masked if rowof_c < lim_lo (query < key)
@@ -2247,7 +2277,6 @@ void attn_dkdv_kernel(BwdParams p) {
           }
         }
       }
-      st.lap<2>();
       if constexpr (DVV) {
         if constexpr (sizeof(E) == 2) {
           const unsigned db = lds_addr(Dc);
@@ -2288,11 +2317,11 @@ void attn_dkdv_kernel(BwdParams p) {
       }
       }
     }
-    st.lap<3>();
+    st.lap<1>();
     wait_vm(tile_pieces * max(0, min(NS - 2, ntiles - 2 - t)));
-    st.lap<4>();
+    st.lap<2>();
     lds_barrier();
-    st.lap<5>();
+    st.lap<3>();
   };
   st.start();
   const int thead = min(ntiles, (BK - 2) / BQ + 1);                  // q0 < kb0 + BK - 1
@@ -2630,11 +2659,14 @@ int launch_dkdv_t(const BwdParams& p, hipStream_t st) {
 // control model's standard attention (N = 1, dv = hs; control.py:38-63).  Head size 96
 // is the reference's own TrainingConfig (n_embd 768, n_head 4: train.py:60-61 with
 // diff_transformer.py:111 gives 768 // 8; the control model's 2 * n_head heads also 96).
+// (A/B variant builds may predefine DTA_FOR_CONFIGS to a subset: faster experiment builds)
+#ifndef DTA_FOR_CONFIGS
 #define DTA_FOR_CONFIGS(X) \
   X(16, 1, 32) X(16, 2, 32) X(16, 3, 32) X(16, 4, 32) X(32, 1, 64) X(32, 2, 64) X(32, 3, 64) X(32, 4, 64) \
   X(64, 1, 128) X(64, 2, 128) X(64, 3, 128) X(64, 4, 128) X(128, 1, 256) X(128, 2, 256) X(128, 3, 256) \
   X(128, 4, 256) X(64, 1, 64) X(128, 1, 128) X(32, 1, 32) \
   X(96, 1, 192) X(96, 2, 192) X(96, 3, 192) X(96, 4, 192) X(96, 1, 96)
+#endif
 
 // whether the N-branch plan of (HS, N, DV) is built for E
 template <class E>

@@ -248,7 +248,8 @@ int dta_attn_fwd(const dta_attn_fwd_args* a, void* stream) {
 // dK/dV launches (branch groups) a backward of this shape runs at the default caps: more than
 // one means dV is summed across groups (in dv_f32 when given)
 int dta_attn_bwd_dkdv_groups(int32_t dtype, int32_t head_size, int32_t n_terms, int32_t dv, int32_t group_max_dkdv) {
-  if (!attn_supported(dtype, head_size, n_terms, dv)) return 0;
+  // a negative cap is invalid here as in dta_attn_bwd
+  if (!attn_supported(dtype, head_size, n_terms, dv) || group_max_dkdv < 0) return 0;
   const int cap = group_max_dkdv > 0 ? group_max_dkdv : bwd_group_cap(dtype, head_size, n_terms, true);
   int n = 0;
   for (int g0 = 0, ng; g0 < n_terms; g0 += ng, ++n) ng = branch_group(dtype, head_size, n_terms - g0, dv, cap);

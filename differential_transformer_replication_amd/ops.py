@@ -121,6 +121,11 @@ def _obr_dtype(dtype: torch.dtype) -> torch.dtype:
     return torch.float32
 
 
+# Whether the backward hands dta_attn_bwd the fp32 dV workspace (ABI 7 dv_f32) when dK/dV runs
+# in more than one branch group.  Always on in the product; the C ABI's other path (dv_f32 NULL:
+# each later group adds into the 16-bit dV) is exercised by the GPU tests with it off.
+_DV_F32_WORKSPACE = [True]
+
 # Backward branch-group caps handed to dta_attn_bwd (ABI 7 group_max_dq / group_max_dkdv);
 # (0, 0) = the library's per-stage defaults.  Tests set them with ``bwd_group_caps`` to run
 # every built native N-branch backward plan.
@@ -129,8 +134,10 @@ _BWD_GROUP_MAX = [0, 0]
 
 @contextlib.contextmanager
 def bwd_group_caps(dq: int, dkdv: int):
-    """Within the block, backward passes run dQ in branch groups of at most ``dq`` and
-    dK/dV in groups of at most ``dkdv`` (0 = the library default for that stage)."""
+    """Forward passes run within the block have their backward run dQ in branch groups of
+    at most ``dq`` and dK/dV in groups of at most ``dkdv`` (0 = the library default for that
+    stage).  The caps are taken at the forward and kept on the autograd context, so the
+    backward may run after the block exits."""
     old = list(_BWD_GROUP_MAX)
     _BWD_GROUP_MAX[:] = [int(dq), int(dkdv)]
     try:
@@ -184,6 +191,9 @@ class _DiffAttention(torch.autograd.Function):
         ctx.save_for_backward(qkv, qk_rot, obr, lse, coef, freqs)
         ctx.dims = (H, N, hs, dv, scale)
         ctx.drop = (dropout_p, seed)
+        # the backward branch-group caps in force at the forward (bwd_group_caps): saved here, so
+        # a backward run after the block exits (or on another thread) uses the same caps
+        ctx.caps = tuple(_BWD_GROUP_MAX)
         return o.view(B, T, H * dv)
 
     @staticmethod
@@ -207,7 +217,8 @@ class _DiffAttention(torch.autograd.Function):
         dcp = torch.empty(lib.dta_attn_bwd_dcoef_partial_bytes(B, T, H, N) // 4, device=dev, dtype=torch.float32)
         # dK/dV in more than one branch group: dV summed in fp32 across the groups (one rounding)
         dv32 = None
-        if dt != _lib.DTA_F32 and lib.dta_attn_bwd_dkdv_groups(dt, hs, N, dv, _BWD_GROUP_MAX[1]) > 1:
+        caps = ctx.caps
+        if dt != _lib.DTA_F32 and _DV_F32_WORKSPACE[0] and lib.dta_attn_bwd_dkdv_groups(dt, hs, N, dv, caps[1]) > 1:
             dv32 = torch.empty(B, T, H, dv, device=dev, dtype=torch.float32)
         # with RoPE the kernels differentiate w.r.t. the rotated Q/K (qk_rot) and their
         # dQ / dK epilogues apply the inverse rotation, writing straight into dqkv
@@ -218,7 +229,7 @@ class _DiffAttention(torch.autograd.Function):
                              _lib.tensor5(dq), _lib.tensor5(dk), _lib.tensor5(dvv),
                              dcoef.data_ptr(), delta.data_ptr(), None, _lib.BWD_PRE,
                              freqs.data_ptr() if freqs is not None else None, dcp.data_ptr(), ctx.drop[1],
-                             _lib.dtype_code(obr.dtype), *_BWD_GROUP_MAX,
+                             _lib.dtype_code(obr.dtype), *caps,
                              dv32.data_ptr() if dv32 is not None else None)
         _lib.check(lib.dta_attn_bwd(a, stream))
         a.stages = _lib.BWD_DQ

@@ -111,6 +111,9 @@ int dta_attn_fwd(const dta_attn_fwd_args* a, void* stream);
  *           to each branch group's first branch, re-based in place where the two stages
  *           group branches differently).  Run DTA_BWD_DQ exactly once per backward and
  *           DTA_BWD_DKDV after it on the same delta; never read or reuse it otherwise.
+ *           When the stages run as separate calls, both calls must pass the SAME
+ *           group_max_dq and group_max_dkdv (the DQ stage encodes delta for the DKDV
+ *           grouping those caps give; different caps in the DKDV call decode it wrongly).
  *   dq_f32  optional fp32 [b][t][h][i][d] contiguous: when dq.ptr is NULL the
  *           dQ kernel writes fp32 here instead (callers that post-process dQ,
  *           e.g. the inverse RoPE, keep full precision). */
@@ -167,7 +170,8 @@ size_t dta_attn_bwd_workspace_bytes(int32_t B, int32_t T, int32_t H, int32_t n_t
                                     int32_t head_size);
 size_t dta_attn_bwd_dcoef_partial_bytes(int32_t B, int32_t T, int32_t H, int32_t n_terms);
 /* The number of dK/dV launches (branch groups) dta_attn_bwd runs for this shape with the given
- * group_max_dkdv (0 = default); 0 if the shape is unsupported.  > 1: pass dv_f32. */
+ * group_max_dkdv (0 = default); 0 if the shape is unsupported or the cap is negative (which
+ * dta_attn_bwd rejects).  > 1: pass dv_f32. */
 int dta_attn_bwd_dkdv_groups(int32_t dtype, int32_t head_size, int32_t n_terms, int32_t dv, int32_t group_max_dkdv);
 
 /* Cross-head LayerNorm x out_scale (GroupLayerNorm.forward,

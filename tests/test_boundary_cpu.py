@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import Golden, ROOT, rel_err
+from conftest import GOLDEN, Golden, ROOT, rel_err
 
 import differential_transformer_replication_amd as dta
 from differential_transformer_replication_amd import _lib
@@ -72,6 +72,10 @@ def test_invalid_args_rejected_without_gpu():
     a.head_size, a.dv = 48, 96
     assert lib.dta_attn_fwd(a, None) == -2
     assert lib.dta_attn_fwd(None, None) == -1
+    # branch-group query: default caps, an explicit cap, and a negative cap (invalid, as in dta_attn_bwd)
+    assert lib.dta_attn_bwd_dkdv_groups(_lib.DTA_BF16, 64, 3, 128, 0) == 2
+    assert lib.dta_attn_bwd_dkdv_groups(_lib.DTA_BF16, 64, 3, 128, 4) == 1
+    assert lib.dta_attn_bwd_dkdv_groups(_lib.DTA_BF16, 64, 3, 128, -1) == 0
 
 
 def test_decode_misaligned_views_rejected_without_gpu():
@@ -151,6 +155,21 @@ def test_model_state_dict_keys(golden):
         ours = {k for k in m.state_dict() if not k.endswith("tril")}
         assert ours == set(g.state_dict().keys()), case
         m.load_state_dict(g.state_dict(torch.float32), strict=True)
+
+
+@pytest.mark.parametrize("key", ["alt3", "diff"])
+def test_seeded_init_matches_reference_diff_models(key):
+    """The bf16 curve fixtures' models (tests/golden/make_curve_golden_bf16.py): same seed ->
+    the same initial state as the reference's, every floating state_dict entry by (sum, sum of
+    squares) in sorted key order, so the GPU replay starts where the reference did."""
+    z = np.load(os.path.join(GOLDEN, "golden_loss_curve_diffmodels.npz"))
+    torch.manual_seed(1337)
+    m = (ND.AlternatingDiffTransformer(12000, 384, 3, 4, 256, 0.0, n_terms=3) if key == "alt3"
+         else D.DiffTransformer(12000, 512, 4, 4, 256, 0.0))
+    sd = {k: v for k, v in m.state_dict().items() if v.is_floating_point()}
+    assert sorted(sd) == list(z[key + "/init_keys"])
+    got = np.array([[float(sd[k].double().sum()), float((sd[k].double() ** 2).sum())] for k in sorted(sd)])
+    np.testing.assert_array_equal(got, z[key + "/init_sums"])
 
 
 def test_seeded_init_matches_reference(golden_curve):

@@ -345,3 +345,59 @@ def test_cfg1_fp16_gradscaler_curve_overlays_reference():
     assert np.isfinite(losses).all()
     assert rel.max() < 2e-2, (int(rel.argmax()), float(rel.max()))
     assert rel.mean() < 5e-3, float(rel.mean())
+
+
+@pytest.mark.parametrize("key", ["alt3", "diff"])
+def test_bf16_curve_overlays_reference(key):
+    """The differential models the benches train (cfg3's AlternatingDiffTransformer with
+    n_terms=3, cfg4's DiffTransformer; small shapes, head size 64), 50 optimizer steps of the
+    reference's loop (train.py:236-281: AdamW, CosineWarmupScheduler, clip 1.0) under bf16
+    autocast on the HIP path, against the reference's fp32 curve of the same seed and data
+    (tests/golden/make_curve_golden_bf16.py).  Tolerance, per step |ours - ref32| / ref32:
+    max <= 2e-2 (north_star's bf16 bar), and mean <= max(5e-3, 2x the reference's own
+    bf16-autocast drift from its fp32 curve, recorded in the same fixture)."""
+    from differential_transformer_replication_amd.train import CosineWarmupScheduler
+    z = np.load(os.path.join(GOLDEN, "golden_loss_curve_diffmodels.npz"))
+    p = key + "/"
+    mb, T, steps, warm = (int(v) for v in z[p + "meta"])
+    torch.manual_seed(1337)
+    model = (ND.AlternatingDiffTransformer(12000, 384, 3, 4, 256, 0.0, n_terms=3) if key == "alt3"
+             else D.DiffTransformer(12000, 512, 4, 4, 256, 0.0))
+    sd = {k: v for k, v in model.state_dict().items() if v.is_floating_point()}
+    assert sorted(sd) == list(z[p + "init_keys"])
+    init = np.array([[float(sd[k].double().sum()), float((sd[k].double() ** 2).sum())] for k in sorted(sd)])
+    np.testing.assert_array_equal(init, z[p + "init_sums"])
+    model = model.to(DEV)
+    opt = torch.optim.AdamW(model.parameters(), lr=3.2e-4, betas=(0.9, 0.95), weight_decay=0.1)
+    sched = CosineWarmupScheduler(opt, warm, steps, 6e-5)
+    toks = torch.from_numpy(z[p + "toks"].astype(np.int64)).to(DEV)
+    offs = z[p + "offs"]
+    losses, lrs = [], []
+    model.train()
+    for s in range(steps):
+        X = torch.stack([toks[o:o + T] for o in offs[s].tolist()])
+        Y = torch.stack([toks[o + 1:o + T + 1] for o in offs[s].tolist()])
+        lrs.append(opt.param_groups[0]["lr"])
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            _, loss = model(X, Y)
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+        sched.step()
+        losses.append(float(loss))
+    np.testing.assert_allclose(lrs, z[p + "lrs"], rtol=1e-6)
+    losses = np.array(losses)
+    ref32, ref16 = z[p + "losses"], z[p + "bf16_losses"]
+    rel = np.abs(losses - ref32) / np.abs(ref32)
+    ref_drift = np.abs(ref16 - ref32) / np.abs(ref32)
+    log = os.environ.get("DTA_TEST_LOG_DIR")
+    if log:
+        import json
+        with open(os.path.join(log, f"bf16_curve_{key}.json"), "w") as fh:
+            json.dump({"ours_bf16": losses.tolist(), "ref_fp32": ref32.tolist(), "ref_bf16_cpu": ref16.tolist(),
+                       "rel_max": float(rel.max()), "rel_mean": float(rel.mean()),
+                       "ref_drift_max": float(ref_drift.max()), "ref_drift_mean": float(ref_drift.mean())}, fh)
+    assert np.isfinite(losses).all()
+    assert rel.max() <= 2e-2, (int(rel.argmax()), float(rel.max()))
+    assert rel.mean() <= max(5e-3, 2 * ref_drift.mean()), (float(rel.mean()), float(ref_drift.mean()))

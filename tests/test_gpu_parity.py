@@ -98,6 +98,22 @@ def test_native_hs128_n3_sampled_rows(dtype):
                    dtype=dtype, seed=71)
 
 
+# ABI 7 dv_f32 = NULL at the default caps: dK/dV runs in branch groups (16-bit, head size 64,
+# N = 3 / 4: groups of 2) and each later group reads, adds and re-stores the 16-bit dV itself
+# (the per-lane read-add-store epilogue) instead of summing in the fp32 workspace.
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("H,N,hs,T,rope", [(2, 3, 64, 129, False), (1, 4, 64, 200, True), (1, 3, 128, 97, False)])
+def test_core_dv_groups_without_f32_workspace(dtype, H, N, hs, T, rope):
+    ops = _ops()
+    from differential_transformer_replication_amd import _lib
+    assert _lib.load().dta_attn_bwd_dkdv_groups(_lib.dtype_code(dtype), hs, N, 2 * hs, 0) > 1
+    ops._DV_F32_WORKSPACE[0] = False
+    try:
+        _core_case(dtype, H, N, hs, T, rope)
+    finally:
+        ops._DV_F32_WORKSPACE[0] = True
+
+
 # ABI 6 obr_dtype = fp16 (ops: DTA_OBR_F16=1, 16-bit activations): O_i stored as fp16 for the
 # backward's delta_i.  The forward's epilogue then keeps its per-lane stores (the LDS bounce
 # takes fp32 O_i only), so this also covers that path; parity against fp64 at the usual bar.

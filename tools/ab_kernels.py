@@ -42,6 +42,10 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--obr", choices=["f32", "f16"], default="f32", help="O_i storage (ABI 6 obr_dtype)")
     ap.add_argument("--dv", type=int, default=0, help="value width (default 2 * head size; head size for N = 1 control)")
+    ap.add_argument("--mode", choices=["kernel", "step"], default="step",
+                    help="kernel: each kernel REPS times back to back (its inputs stay in the 256 MB Infinity "
+                         "Cache: optimistic for shapes whose operands fit); step: fwd, dq, dkdv in turn per rep, "
+                         "as in a training step and bench.py (default)")
     args = ap.parse_args()
     B, H, hs, N, T = (int(x) for x in args.shape.split(","))
     dv = args.dv or 2 * hs
@@ -128,6 +132,22 @@ def main():
     # order read the first build ~0.1 ms/step slow (profiles/r02_ab_sched_strategy.json)
     for r in range(args.rounds):
         for name, _ in builds[r % len(builds):] + builds[:r % len(builds)]:
+            if args.mode == "step":
+                for w in ("fwd", "pre", "dq", "dkdv"):       # untimed lead step
+                    run(name, w)
+                ev = {w: [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                          for _ in range(args.reps)] for w in ("fwd", "dq", "dkdv")}
+                for i in range(args.reps):
+                    for w in ("fwd", "dq", "dkdv"):
+                        if w == "dq":
+                            run(name, "pre")
+                        ev[w][i][0].record()
+                        run(name, w)
+                        ev[w][i][1].record()
+                torch.cuda.synchronize()
+                for w in ("fwd", "dq", "dkdv"):
+                    res[name][w].extend(a.elapsed_time(b) for a, b in ev[w])
+                continue
             for w in ("fwd", "dq", "dkdv"):
                 if w == "dq":
                     run(name, "pre")
@@ -158,7 +178,7 @@ def main():
         out[name] = {"median_ms": {w: round(x, 4) for w, x in med.items()},
                      "min_ms": {w: round(x, 4) for w, x in mn.items()},
                      "sum_median_ms": round(sum(med.values()), 4), "rel_diff_vs_" + base: diff}
-    print(json.dumps({"shape": dict(B=B, H=H, hs=hs, N=N, T=T), "rounds": args.rounds, "reps": args.reps,
+    print(json.dumps({"shape": dict(B=B, H=H, hs=hs, N=N, T=T), "mode": args.mode, "rounds": args.rounds, "reps": args.reps,
                       "builds": out}, indent=1))
 
 

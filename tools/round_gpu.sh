@@ -37,6 +37,7 @@ if [ -n "$SQ" ]; then
     i=$((i+1))
     timeout -s KILL 120 rocprofv3 --pmc $grp --output-format csv -d $OUT/sq$i -o run -- python3 $R/bench.py $PC --no-hbm --steps 2 --warmup 1 > $OUT/sq$i.log 2>&1 || { echo "SQ group $i failed"; tail -5 $OUT/sq$i.log; exit 1; }
   done
-  python3 $R/tools/pmc_sq.py $OUT/sq1 $OUT/sq2 --json $OUT/sq.json > $OUT/sq_summary.txt && cat $OUT/sq_summary.txt
+  LSHA=$(sha256sum $R/differential_transformer_replication_amd/lib/libdiffattn.so | cut -c1-16)
+  python3 $R/tools/pmc_sq.py $OUT/sq1 $OUT/sq2 --json $OUT/sq.json --lib-sha $LSHA --shape B8_H16_hs64_N2_T4096_dv128 > $OUT/sq_summary.txt && cat $OUT/sq_summary.txt
 fi
 echo ROUND_GPU_OK

@@ -20,7 +20,8 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 from differential_transformer_replication_amd import _lib  # noqa: E402
 
 FWD_SEGS = ["dma_issue", "qk_softmax", "pv", "wait_vm", "barrier", "tail", "-", "loop_top"]
-DKDV_SEGS = ["dma_issue", "dP", "branches(S,dS,dK)", "dV", "wait_vm", "barrier", "-", "-"]
+DKDV_SEGS = ["dma_issue", "compute(dP,S,dS,dK,dV)", "wait_vm", "barrier", "-", "-", "-", "-"]
+DQ_SEGS = ["dma_issue", "dP", "branches(S,dS,dQ)", "wait_vm", "barrier", "-", "-", "-"]
 
 
 def main():
@@ -66,7 +67,9 @@ def main():
                           delta.data_ptr(), None, 0, None)
     out = {}
     nbytes = 8 << 20
-    for which in ("fwd", "dkdv"):
+    for which in ("fwd", "dq", "dkdv"):
+        # dq: the PRE + DQ stages only (the DKDV stage would overwrite the per-wave slots)
+        ba.stages = _lib.BWD_PRE | _lib.BWD_DQ if which == "dq" else 0
         for _ in range(30):                      # >= 2 s of back-to-back launches would be ideal; shares only
             assert (lib.dta_attn_fwd(fa, stream) if which == "fwd" else lib.dta_attn_bwd(ba, stream)) == 0
         torch.cuda.synchronize()
@@ -74,7 +77,7 @@ def main():
         assert lib.dta_debug_stamps(buf.ctypes.data, nbytes) == 0
         st = buf.reshape(-1, 8)
         st = st[st.sum(1) > 0].astype(np.float64)
-        names = FWD_SEGS if which == "fwd" else DKDV_SEGS
+        names = {"fwd": FWD_SEGS, "dq": DQ_SEGS, "dkdv": DKDV_SEGS}[which]
         tot = st.sum(0)
         out[which] = {"waves": int(st.shape[0]),
                       "share": {n: round(float(x / tot.sum()), 4) for n, x in zip(names, tot) if n != "-"},
