@@ -514,14 +514,42 @@ def hbm_bench(reps=20):
 
 
 def train_leg(args, world, rank):
-    """BASELINE configs[3] DP training step (cfg4) at this run's world size."""
+    """BASELINE configs[3] DP training step (cfg4) at this run's world size.  At one GPU the
+    step launches no collective; it then runs a second time over a 1-rank RCCL process group
+    with every gradient bucket's all-reduce launched from the backward hooks
+    (BucketedAllReduce(reduce_single=True)): the difference is the hook / launch / RCCL
+    overhead an N-rank step carries on top of its xGMI transfer time."""
     from differential_transformer_replication_amd.train import train_bench
     targs = argparse.Namespace(steps=args.train_steps, warmup=args.train_warmup, model="diff",
                                n_terms=args.n_terms, device=args.device)
     r = train_bench(targs, world, rank)
     keep = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "final_loss", "config",
             "model_tflops", "mfu")
-    return {k: r[k] for k in keep if k in r}
+    out = {k: r[k] for k in keep if k in r}
+    if world == 1 and args.device == "cuda" and args.rccl_world1:
+        torch.cuda.empty_cache()
+        own = not dist.is_initialized()
+        try:
+            if own:
+                import socket
+                with socket.socket() as sk:
+                    sk.bind(("127.0.0.1", 0))
+                    port = sk.getsockname()[1]
+                dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                                        device_id=torch.device("cuda", torch.cuda.current_device()))
+            r1 = train_bench(argparse.Namespace(**vars(targs), reduce_single=True), 1, 0)
+            out["rccl_hooks_world1"] = {
+                "what": "the same cfg4 step with every bucket all-reduce launched from the backward hooks over a "
+                        "1-rank RCCL group (no xGMI traffic): hook + launch + RCCL overhead per step",
+                "value": r1["value"], "ms_per_step": r1["ms_per_step"],
+                "overhead_ms": round(r1["ms_per_step"] - r["ms_per_step"], 3),
+                "parallelism": r1["config"]["parallelism"]}
+        except Exception as e:          # report, never fail the bench line over the probe
+            out["rccl_hooks_world1"] = {"error": f"{type(e).__name__}: {e}"[:300]}
+        finally:
+            if own and dist.is_initialized():
+                dist.destroy_process_group()
+    return out
 
 
 def run(args):
@@ -604,6 +632,8 @@ def main():
     ap.add_argument("--train-steps", type=int, default=8,
                     help="kernel mode: timed steps of the cfg4 DP training leg (0 = skip)")
     ap.add_argument("--train-warmup", type=int, default=3)
+    ap.add_argument("--no-rccl-world1", dest="rccl_world1", action="store_false",
+                    help="kernel mode, one GPU: skip the second cfg4 train leg over a 1-rank RCCL group")
     ap.add_argument("--no-hbm", dest="hbm", action="store_false", help="kernel mode: skip the LN / RoPE timings")
     ap.add_argument("--no-configs", dest="configs", action="store_false",
                     help="kernel mode: skip the cfg3 / cfg5 legs (one GPU only)")

@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get("DTA_LIB", os.path.join(_HERE, "lib", "libdiffattn.so"
 DTA_BF16, DTA_F16, DTA_F32 = 0, 1, 2
 _DTYPES = {torch.bfloat16: DTA_BF16, torch.float16: DTA_F16, torch.float32: DTA_F32}
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 # every symbol include/diffattn.h declares
 EXPORTS = ("dta_attn_fwd", "dta_attn_bwd", "dta_attn_bwd_workspace_bytes", "dta_attn_bwd_dcoef_partial_bytes",
@@ -66,7 +66,7 @@ class AttnBwdArgs(ctypes.Structure):
                 ("stages", ctypes.c_int32), ("rope_freqs", ctypes.c_void_p), ("dcoef_partial", ctypes.c_void_p),
                 ("dropout_seed", ctypes.c_uint64), ("obr_dtype", ctypes.c_int32),
                 ("group_max_dq", ctypes.c_int32), ("group_max_dkdv", ctypes.c_int32),
-                ("dv_f32", ctypes.c_void_p)]
+                ("dv_f32", ctypes.c_void_p), ("lse_c", ctypes.c_void_p)]
 
 
 BWD_PRE, BWD_DQ, BWD_DKDV = 1, 2, 4

@@ -638,6 +638,12 @@ inline bool kv_layout_ok(const P& p, int es) {
 #ifndef DTA_FWD_PIPE
 #define DTA_FWD_PIPE 3
 #endif
+#ifndef DTA_FWD_TR_EARLY
+#define DTA_FWD_TR_EARLY 0       // A/B: the forward's first d-block V^T reads issued before the last softmax
+#endif
+#ifndef DTA_FWD_SEED
+#define DTA_FWD_SEED 0           // A/B: forward Q_i pre-scaled by scale*log2e, S seeded with -m by one MFMA (FAST tiles)
+#endif
 #ifndef DTA_FWD_FAST
 #define DTA_FWD_FAST 1
 #endif
@@ -897,6 +903,19 @@ void attn_fwd_kernel(FwdParams p) {
       }
   }
 
+  // FSEED (see below; the same condition as FAST): the register-resident Q_i pre-scaled by
+  // scale*log2e once, after the RoPE'd rows went to qrot; the LDS-resident ones after they land
+  constexpr bool FSEED_Q = DTA_FWD_SEED && DTA_FWD_FAST && sizeof(E) == 2 && !DROP && N <= 2 &&
+                           (CF::PAIR || CF::WPE >= 2);
+  if constexpr (FSEED_Q) {
+#pragma unroll
+    for (int i = 0; i < NQR; ++i)
+#pragma unroll
+      for (int s = 0; s < NSQ; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) qf[i][s][j] = (E)((float)qf[i][s][j] * p.sl2);
+  }
+  bool q_lds_unscaled = FSEED_Q && N > NQR;
   const int kend = min(T, q0 + BM);
   const int ntiles = (kend + BN - 1) / BN;
   using KR = KvRing<E, HS, N, DVC, BN, NW>;
@@ -934,6 +953,19 @@ void attn_fwd_kernel(FwdParams p) {
   constexpr bool FAST = DTA_FWD_FAST && sizeof(E) == 2 && !DROP && N <= 2 && (CF::PAIR || CF::WPE >= 2);
   constexpr float LSMAX = std::is_same<E, _Float16>::value ? 0x1p15f : 0x1p60f;
   float bad = 0.f;
+  // SEED (with FAST): Q_i are pre-scaled by scale*log2e once (registers and LDS), so scores come
+  // out of QK^T in log2 units, and on the fixed-reference tiles each branch's S accumulators
+  // start at -m by one extra MFMA (a ones fragment times the row constant split into hi + lo
+  // halves, as in attn_dq): P = exp2(S) needs no fma.  Every m is kept at a value the two halves
+  // represent exactly, so the first tile, the seeded tiles and the LSE agree.
+  constexpr bool FSEED = DTA_FWD_SEED && FAST;
+  static_assert(FSEED == FSEED_Q, "FSEED_Q restates FAST's condition");
+  typename O::frag f_one = O::zero(), f_nm[FSEED ? N : 1];
+  if constexpr (FSEED) { if (hf == 0) { f_one[0] = (E)1.f; f_one[1] = (E)1.f; } }
+  auto mrep = [](float v) -> float {     // nearest value hi + lo (two E halves) represent
+    const E hi = (E)v;
+    return (float)hi + (float)(E)(v - (float)hi);
+  };
 
   // per-lane LDS read bases kept in registers across the loop (see attn_dkdv_kernel)
   int LrK = 0, LtV = 0;      // set per attempt, after the ring prologue
@@ -959,15 +991,17 @@ void attn_fwd_kernel(FwdParams p) {
   };
   // P = exp2(S * scale*log2e - m), row sums (two chains), packed to the PV operand;
   // with dropout the row sum keeps every element and the PV operand only the kept ones
-  auto exp_pack = [&](int i, int k0, f32x16 (&sa)[NKB], frag (&pf)[NKB * SPB]) -> float {
+  auto exp_pack = [&](int i, int k0, f32x16 (&sa)[NKB], frag (&pf)[NKB * SPB], bool seeded = false) -> float {
     const float mi = m[i];
     float ls0 = 0.f, ls1 = 0.f;
+    // FSEED: scores already in log2 units (seeded tiles: already minus m)
+    auto arg = [&](float v) { return FSEED ? (seeded ? v : v - mi) : fmaf(v, p.sl2, -mi); };
 #pragma unroll
     for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
       for (int r = 0; r < 16; r += 2) {
-        const float e0 = exp2_fast(fmaf(sa[kb][r], p.sl2, -mi));
-        const float e1 = exp2_fast(fmaf(sa[kb][r + 1], p.sl2, -mi));
+        const float e0 = exp2_fast(arg(sa[kb][r]));
+        const float e1 = exp2_fast(arg(sa[kb][r + 1]));
         sa[kb][r] = e0;
         sa[kb][r + 1] = e1;
         ls0 += e0;
@@ -1001,14 +1035,14 @@ void attn_fwd_kernel(FwdParams p) {
     if constexpr (decltype(MASKED)::value) mask_scores(k0, sa);
     if constexpr (decltype(FASTT)::value) {
       {
-        const float ls = exp_pack(i, k0, sa, pf);
+        const float ls = exp_pack(i, k0, sa, pf, FSEED);
         bad = (ls <= LSMAX) ? bad : 1.f;        // NaN / inf / past the operand range: re-run
         return;
       }
     }
-    const float mx = wave_max_halves(row_max(sa)) * p.sl2;
+    const float mx = wave_max_halves(row_max(sa)) * (FSEED ? 1.f : p.sl2);
     if (__any(mx > m[i] + THR)) {
-      const float mnew = fmaxf(m[i], mx);
+      const float mnew = FSEED ? mrep(fmaxf(m[i], mx)) : fmaxf(m[i], mx);
       const float alpha = exp2_fast(m[i] - mnew);
       m[i] = mnew;
       l[i] *= alpha;
@@ -1016,6 +1050,19 @@ void attn_fwd_kernel(FwdParams p) {
       for (int d = 0; d < NDB; ++d) acc[i][d] *= alpha;
     }
     exp_pack(i, k0, sa, pf);
+  };
+  // DTA_FWD_TR_EARLY (single-branch 16-bit plans without dropout -- the N = 2 plan spills with it --
+  // on the non-pipelined PV path): the first d-block's V^T
+  // reads of the PV product are issued after the last branch's QK^T chain, ahead of its softmax
+  // VALU, so their LDS latency hides behind it (16 more VGPRs live across it)
+  constexpr bool FTRE = DTA_FWD_TR_EARLY && N == 1 && sizeof(E) == 2 && !DROP && !(DTA_FWD_PIPE > 0 && NKB == 1 && NDB > 1);
+  lds64 rv0[NKB][4];        // (full size even when unused: referenced in a generic lambda)
+  auto issue_v0 = [&](int kt) {
+    if constexpr (FTRE) {
+      const unsigned vb = lds_addr(Vb + (kt % NS) * CF::nV);
+      const unsigned a0 = vb + LtV, a1 = vb + (LtV ^ 32);
+      sfor<NKB>([&](auto KB) { tr_issue<VI::ROWB, 32 * decltype(KB)::value>(rv0[decltype(KB)::value], a0, a1); });
+    }
   };
   // QK^T + online softmax of one key tile for every branch, P packed as the PV B operand
   auto phase_a = [&](int kt, auto MASKED, frag (&pf)[N][NKB * SPB], auto FASTT) {
@@ -1033,7 +1080,8 @@ void attn_fwd_kernel(FwdParams p) {
         const char* kbase = reinterpret_cast<const char*>(Ki);
         const char* qbase = reinterpret_cast<const char*>(Qs + (i >= NQR ? i - NQR : 0) * BM * HSP) + wave * 32 * QI::ROWB;
 #pragma unroll
-        for (int kb = 0; kb < NKB; ++kb) sa[i][kb] = f32x16{};
+        for (int kb = 0; kb < NKB; ++kb)
+          sa[i][kb] = (FSEED && decltype(FASTT)::value) ? O::mma(f_one, f_nm[FSEED ? i : 0], f32x16{}) : f32x16{};
         if constexpr (NSQ * (NKB + 1) <= 12 && QRH == 0) {
           // every operand read of this branch's S^T issued ahead of its MFMA chain,
           // so the chain waits on the LDS latency once instead of per k-step
@@ -1090,6 +1138,7 @@ void attn_fwd_kernel(FwdParams p) {
           }
         }
       }
+      if (FTRE && i == N - 1) issue_v0(kt);
       softmax_branch(i, k0, MASKED, sa[i], pf[i], FASTT);
     }
   };
@@ -1130,6 +1179,18 @@ void attn_fwd_kernel(FwdParams p) {
         constexpr int d = decltype(D)::value;
         lds64 r[NKB][4];
         const unsigned a0 = vb + (Lv ^ (64 * d)), a1 = vb + (Lv ^ (64 * d + 32));
+        if constexpr (FTRE && d == 0) {
+          lgkm_pin<NKB>(rv0);
+#pragma unroll
+          for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+              const frag va = tr_frag<E>(rv0[kb], s);
+#pragma unroll
+              for (int i = 0; i < N; ++i) acc[i][d] = O::mma(va, pf[i][kb * 2 + s], acc[i][d]);
+            }
+          return;
+        }
         if constexpr (SPILLS) {
           sfor<NKB>([&](auto KB) { tr_load<VI::ROWB, 32 * decltype(KB)::value>(r[decltype(KB)::value], a0, a1); });
         } else {
@@ -1202,6 +1263,11 @@ void attn_fwd_kernel(FwdParams p) {
       lds_barrier();
       qrot_pending = false;
     }
+    if (q_lds_unscaled) {                    // FSEED: the LDS-resident Q_i, once
+      scale_lds<E, NTHR>(Qs, CF::nQ, p.sl2, tid);
+      lds_barrier();
+      q_lds_unscaled = false;
+    }
 #pragma unroll
     for (int i = 0; i < N; ++i) {
       m[i] = -INFINITY;
@@ -1217,6 +1283,10 @@ void attn_fwd_kernel(FwdParams p) {
     for (int kt = 0; kt < min(nfull, kslow); ++kt) step(kt, std::false_type{}, std::false_type{});
     for (int kt = nfull; kt < kslow; ++kt) step(kt, std::true_type{}, std::false_type{});
     if constexpr (FAST) {
+      if constexpr (FSEED) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) f_nm[i] = seed_frag<E>(-m[i], hf);     // m[i] = hi + lo exactly
+      }
       for (int kt = kslow; kt < nfull; ++kt) step(kt, std::false_type{}, std::true_type{});
       for (int kt = max(kslow, nfull); kt < ntiles; ++kt) step(kt, std::true_type{}, std::true_type{});
     }
@@ -1374,6 +1444,15 @@ struct DqCfg {
 #ifndef DTA_DQ_PAIR3
 #define DTA_DQ_PAIR3 1
 #endif
+#ifndef DTA_DQ_TR_EARLY
+#define DTA_DQ_TR_EARLY 0        // A/B: dQ's first d-block transposed K_i reads issued before the softmax VALU
+#endif
+#ifndef DTA_DKDV_TR_EARLY
+#define DTA_DKDV_TR_EARLY 0      // A/B: dK/dV's transposed Q_i reads issued before the softmax VALU
+#endif
+#ifndef DTA_DKDV_CFOLD
+#define DTA_DKDV_CFOLD 1         // 0: never build the |c_i|-folded dK/dV instantiations (lse_c ignored)
+#endif
 #ifndef DTA_DQ_EARLY_RING
 #define DTA_DQ_EARLY_RING 0      // A/B: the K/V ring's first stages issued before the delta_i prologue
 #endif
@@ -1502,6 +1581,9 @@ void attn_dq_kernel(BwdParams p) {
       }
     }
     lse[i] = rowok ? p.lse[rs + i * bstride] : 0.f;
+    // ABI 8 lse_c: the stored LSE_i + log2|c_i| for attn_dkdv, which then seeds its scores with
+    // it and gets |c_i| P_i out of its exp (c_i = 0: -inf, P = 0)
+    if (p.lsec && rowok && hf == 0) p.lsec[rs + i * bstride] = lse[i] + __builtin_log2f(fabsf(coef[i]));
     // delta_i = <dO, O_i> over this row (flash-backward preprocess), both lane halves
     float d = 0.f;
     if (rowok) {
@@ -1703,6 +1785,16 @@ void attn_dq_kernel(BwdParams p) {
               }
             }
           }
+          // DTA_DQ_TR_EARLY: the first d-block's transposed K_i reads of dQ_i issued here, ahead
+          // of the softmax VALU below (16 more VGPRs live across it)
+          constexpr bool TRE = DTA_DQ_TR_EARLY && sizeof(E) == 2 && !SPILLS;
+          lds64 rk0[NKB][4];      // (full size even when unused: referenced in a generic lambda)
+          if constexpr (TRE) {
+            const unsigned kbse = lds_addr(Ki);
+            const unsigned a0 = XA ? tK + (unsigned)(i * BN * HSP * (int)sizeof(E)) : kbse + LtK;
+            const unsigned a1 = XA ? (tK ^ 32) + (unsigned)(i * BN * HSP * (int)sizeof(E)) : kbse + (LtK ^ 32);
+            sfor<NKB>([&](auto KB) { tr_issue<KI::ROWB, 32 * decltype(KB)::value>(rk0[decltype(KB)::value], a0, a1); });
+          }
           // dS^T = c_i P^T (dP^T - delta_i) = P^T * (c_i dP^T - c_i delta_i)
           const float li = lse[i], ci = coef[i], cdi = coef[i] * del[i];
           const int lim = min(qrow, T - 1) - k0 - 4 * hf;
@@ -1755,6 +1847,15 @@ void attn_dq_kernel(BwdParams p) {
               const unsigned a0 = XA ? (tK ^ (64 * d)) + (unsigned)(i * BN * HSP * (int)sizeof(E)) : kbse + (Lk ^ (64 * d));
               const unsigned a1 = XA ? (tK ^ (64 * d + 32)) + (unsigned)(i * BN * HSP * (int)sizeof(E))
                                      : kbse + (Lk ^ (64 * d + 32));
+              if constexpr (TRE && d == 0) {
+                lgkm_pin<NKB>(rk0);
+#pragma unroll
+                for (int kb = 0; kb < NKB; ++kb) {
+                  dq[i][d] = O::mma(tr_frag<E>(rk0[kb], 0), O::template pack<0>(sa[kb]), dq[i][d]);
+                  dq[i][d] = O::mma(tr_frag<E>(rk0[kb], 1), O::template pack<1>(sa[kb]), dq[i][d]);
+                }
+                return;
+              }
               if constexpr (SPILLS) {
                 sfor<NKB>([&](auto KB) { tr_load<KI::ROWB, 32 * decltype(KB)::value>(r[decltype(KB)::value], a0, a1); });
               } else {
@@ -1989,7 +2090,8 @@ struct DkdvWaves {
   static constexpr int v = !gr ? v0 : (DkdvCfg<E, HS, N, DV, 2, false, true>::bytes <= LIM ? 2 : 1);
 };
 
-template <class E, int HS, int N, int DV, int NW, bool DK, bool DVV, bool SRD, bool DROP, bool PR, bool GRX>
+template <class E, int HS, int N, int DV, int NW, bool DK, bool DVV, bool SRD, bool DROP, bool PR, bool GRX,
+          bool CFOLD = false>
 __global__ __launch_bounds__(NW * 64, (NW >= 8 || PR ? 2 : 1))
 void attn_dkdv_kernel(BwdParams p) {
   using O = Ops<E>;
@@ -2048,6 +2150,17 @@ void attn_dkdv_kernel(BwdParams p) {
     coef[i] = p.coef[hh * p.cst + i];
     dkey[i] = DROP ? drop_key(p.drop_seed_lo, p.drop_seed_hi, b, hh, p.br0 + i, p.H, p.cst) : 0u;
   }
+  // CFOLD (ABI 8 lse_c, 16-bit, no dropout): the S seeds are the stored LSE_i + log2|c_i| rows
+  // attn_dq wrote, so exp gives P~_i = |c_i| P_i.  dV's operand sum_i c_i P_i = s_0 (P~_0 +
+  // sum_{i>=1} s_0 s_i P~_i) with s_i = sign(c_i): branch 0 needs no multiply, the dV epilogue
+  // takes s_0; dS_i is accumulated as P~_i (dP - delta_i), so dK_i's epilogue takes s_i, not c_i.
+  static_assert(!CFOLD || (!DROP && sizeof(E) == 2 && !GRX), "CFOLD: 16-bit plans without dropout");
+  auto sgn = [](float c) { return c < 0.f ? -1.f : 1.f; };
+  float wv[N];                        // pc weights: c_i, or s_0 s_i (CFOLD)
+#pragma unroll
+  for (int i = 0; i < N; ++i) wv[i] = CFOLD ? sgn(coef[0]) * sgn(coef[i]) : coef[i];
+  const float dvsc = CFOLD ? sgn(coef[0]) : 1.f;    // dV epilogue factor
+  const float* lsep = CFOLD ? p.lsec : p.lse;
   // this wave's key rows of every K_i and of V as B fragments
   // this wave's V rows as B fragments of dP = dO V^T (registers); K_i rows live in LDS
   frag vf[DK ? NSV : 1];
@@ -2062,14 +2175,14 @@ void attn_dkdv_kernel(BwdParams p) {
   if constexpr (SRD) RG::offsets(p, bstride, wave, lane, roff);
   auto stage_q = [&](int q0, int buf) {
     if constexpr (SRD) {
-      RG::issue_pre(p, gq, gdo, p.lse + rowvec, p.delta + rowvec, bstride, q0, T, ringb + buf * RG::SB, wave, roff);
+      RG::issue_pre(p, gq, gdo, lsep + rowvec, p.delta + rowvec, bstride, q0, T, ringb + buf * RG::SB, wave, roff);
     } else {
 #pragma unroll
       for (int i = 0; i < N; ++i)
         stage<E, HSP, BQ, HS, NTHR>(Qb + (buf * N + i) * BQ * HSP, gq + i * p.q.si, p.q.st, q0, T - 1, tid);
       stage<E, DVP, BQ, DV, NTHR>(Db + buf * CF::nD, gdo, p.dout.st, q0, T - 1, tid);
       if constexpr (!GR) {
-        stage_rows<N, BQ, NTHR>(Lb + buf * NP, p.lse + rowvec, bstride, q0, T - 1, tid);
+        stage_rows<N, BQ, NTHR>(Lb + buf * NP, lsep + rowvec, bstride, q0, T - 1, tid);
         if constexpr (DK) stage_rows<N, BQ, NTHR>(Gb + buf * NP, p.delta + rowvec, bstride, q0, T - 1, tid);
       }
     }
@@ -2192,11 +2305,14 @@ void attn_dkdv_kernel(BwdParams p) {
       const int lim_hi = T - 1 - q0 - 4 * hf;         // masked if rowof_c > lim_hi (query >= T)
 #pragma unroll
       for (int i = 0; i < N; ++i) {
+        // CFOLD: keep the branches in program order (with branch 0's dV operand free of a multiply
+        // the scheduler otherwise hoists the next branch's score chain and spills)
+        if constexpr (CFOLD) if (i > 0) __builtin_amdgcn_sched_barrier(0);
         // S'_i accumulator seeded with the -LSE rows (K_i is pre-scaled by sl2)
         f32x16 sa;
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          const f32x4 l4 = rows4(Lc, p.lse, i, g);
+          const f32x4 l4 = rows4(Lc, lsep, i, g);
 #pragma unroll
           for (int j = 0; j < 4; ++j) sa[4 * g + j] = l4[j];
         }
@@ -2222,6 +2338,19 @@ void attn_dkdv_kernel(BwdParams p) {
           for (int s = 0; s < NSQ; ++s)
             sa = O::mma(QI::row(Qi, c32, s, hf), KI::row(Ks + i * BK * KP, wave * 32 + c32, s, hf), sa);
         }
+        // DTA_DKDV_TR_EARLY: the transposed Q_i reads of dK_i issued here, ahead of the softmax
+        // VALU below, so their LDS latency hides behind it (16 more VGPRs live across it)
+        constexpr bool TRE = DTA_DKDV_TR_EARLY && DK && sizeof(E) == 2 && !SPILLS;
+        lds64 rq[TRE ? NHB : 1][4];
+        if constexpr (TRE) {
+          const unsigned qb = lds_addr(Qi);
+          const int Lq = LtQ;
+          sfor<NHB>([&](auto D) {
+            constexpr int d = decltype(D)::value;
+            if constexpr (XA) tr_issue<QI::ROWB, 0>(rq[d], (tQ ^ (64 * d)) + i * RG::QB, (tQ ^ (64 * d + 32)) + i * RG::QB);
+            else tr_issue<QI::ROWB, 0>(rq[d], qb + (Lq ^ (64 * d)), qb + (Lq ^ (64 * d + 32)));
+          });
+        }
         // sa[r] = S'_i[q0 + rowof(r)][krow] - LSE; rows 4g..4g+3 of a lane are consecutive
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
@@ -2242,12 +2371,20 @@ void attn_dkdv_kernel(BwdParams p) {
               if constexpr (DVV) pc[r] = fmaf(coef[i] * mk, pr, pc[r]);
               if constexpr (DK) sa[r] = pr * fmaf(mk, dpa[r], -d4[j]);
             } else {
-              if constexpr (DVV) pc[r] = i == 0 ? coef[0] * pr : fmaf(coef[i], pr, pc[r]);
+              if constexpr (DVV) pc[r] = i == 0 ? (CFOLD ? pr : wv[0] * pr) : fmaf(wv[i], pr, pc[r]);
               if constexpr (DK) sa[r] = i == 0 ? pr * dpa[r] : pr * (dpa[r] + d4[j]);
             }
           }
         }
-        if constexpr (DK) {
+        if constexpr (TRE) {
+          lgkm_pin<NHB>(rq);
+          const frag p0 = O::template pack<0>(sa), p1 = O::template pack<1>(sa);
+#pragma unroll
+          for (int d = 0; d < NHB; ++d) {
+            dk[i][d] = O::mma(tr_frag<E>(rq[d], 0), p0, dk[i][d]);
+            dk[i][d] = O::mma(tr_frag<E>(rq[d], 1), p1, dk[i][d]);
+          }
+        } else if constexpr (DK) {
           if constexpr (sizeof(E) == 2) {
             const unsigned qb = lds_addr(Qi);
             const int Lq = LtQ;
@@ -2347,7 +2484,7 @@ void attn_dkdv_kernel(BwdParams p) {
       if constexpr (DK) {
 #pragma unroll
         for (int i = 0; i < N; ++i) {
-          const float sc = p.scale * coef[i];      // dS_i was accumulated without its c_i
+          const float sc = p.scale * (CFOLD ? sgn(coef[i]) : coef[i]);   // dS_i was accumulated without c_i (CFOLD: |c_i| in)
           bounce_store<E, NHB>(reg, lane, [&](int d, int g) {
             float a0 = dk[i][d][4 * g] * sc, a1 = dk[i][d][4 * g + 1] * sc;
             float a2 = dk[i][d][4 * g + 2] * sc, a3 = dk[i][d][4 * g + 3] * sc;
@@ -2359,7 +2496,9 @@ void attn_dkdv_kernel(BwdParams p) {
       }
       if constexpr (DVV) {
         if (!p.dv_acc) {
-          auto val = [&](int d, int g) { return f32x4{dv[d][4 * g], dv[d][4 * g + 1], dv[d][4 * g + 2], dv[d][4 * g + 3]}; };
+          auto val = [&](int d, int g) {
+            return f32x4{dv[d][4 * g] * dvsc, dv[d][4 * g + 1] * dvsc, dv[d][4 * g + 2] * dvsc, dv[d][4 * g + 3] * dvsc};
+          };
           if (to32) bounce_store<float, NVB>(reg, lane, val, g32, (int64_t)p.H * p.DV, nrows);
           else bounce_store<E, NVB>(reg, lane, val, reinterpret_cast<E*>(p.dv.p) + b * p.dv.sb + (int64_t)kw0 * p.dv.st +
                                                        hh * p.dv.sh, p.dv.st, nrows);
@@ -2377,7 +2516,8 @@ void attn_dkdv_kernel(BwdParams p) {
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int e = d * 32 + 8 * g + 4 * hf;
-          float a0 = dv[d][4 * g], a1 = dv[d][4 * g + 1], a2 = dv[d][4 * g + 2], a3 = dv[d][4 * g + 3];
+          float a0 = dv[d][4 * g] * dvsc, a1 = dv[d][4 * g + 1] * dvsc, a2 = dv[d][4 * g + 2] * dvsc,
+                a3 = dv[d][4 * g + 3] * dvsc;
           if (g32r) {
             const f32x4 v = *reinterpret_cast<const f32x4*>(g32r + e);
             a0 += v[0]; a1 += v[1]; a2 += v[2]; a3 += v[3];
@@ -2395,7 +2535,7 @@ void attn_dkdv_kernel(BwdParams p) {
     E* gdk = reinterpret_cast<E*>(p.dk.p) + b * p.dk.sb + (int64_t)krow * p.dk.st + hh * p.dk.sh;
 #pragma unroll
     for (int i = 0; i < N; ++i) {
-      const float sc = p.scale * coef[i];      // dS_i was accumulated without its c_i
+      const float sc = p.scale * (CFOLD ? sgn(coef[i]) : coef[i]);   // dS_i was accumulated without c_i (CFOLD: |c_i| in)
 #pragma unroll
       for (int d = 0; d < NHB; ++d)
 #pragma unroll
@@ -2421,7 +2561,8 @@ void attn_dkdv_kernel(BwdParams p) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int e = d * 32 + 8 * g + 4 * hf;
-        float a0 = dv[d][4 * g], a1 = dv[d][4 * g + 1], a2 = dv[d][4 * g + 2], a3 = dv[d][4 * g + 3];
+        float a0 = dv[d][4 * g] * dvsc, a1 = dv[d][4 * g + 1] * dvsc, a2 = dv[d][4 * g + 2] * dvsc,
+              a3 = dv[d][4 * g + 3] * dvsc;
         if (p.dv_acc) {        // a later branch group: dV = sum over every group's branches
           if (g32) {
             const f32x4 v = *reinterpret_cast<const f32x4*>(g32 + e);
@@ -2630,12 +2771,20 @@ int launch_dkdv_t(const BwdParams& p, hipStream_t st) {
   constexpr int HSB = DkdvSplit<HS, N, DV>::HSB;
   constexpr bool FUSED = DkdvSplit<HS, N, DV>::fused ||
                          (DTA_DKDV_FUSE1 && sizeof(E) == 2 && NW == 4 && !PR && N * HSB / 2 + DV / 2 <= 288);
+  // ABI 8 lse_c (p.lsec): the |c_i|-folded instantiation, built for the 16-bit plans without
+  // dropout whose row vectors ride in the ring
+  constexpr bool CAN_FOLD = sizeof(E) == 2 && !DROP && !GR && DTA_DKDV_CFOLD;
   auto run = [&](auto DKV, auto DVVV, auto SRDV) -> int {
-    auto kern = attn_dkdv_kernel<E, HS, N, DV, NW, decltype(DKV)::value, decltype(DVVV)::value, decltype(SRDV)::value,
-                                 DROP, PR, GR>;
-    if (int e = set_smem(kern, bytes)) return e;
-    hipLaunchKernelGGL(kern, grid, block, bytes, st, p);
-    return 0;
+    auto launch = [&](auto CFV) -> int {
+      auto kern = attn_dkdv_kernel<E, HS, N, DV, NW, decltype(DKV)::value, decltype(DVVV)::value,
+                                   decltype(SRDV)::value, DROP, PR, GR, decltype(CFV)::value>;
+      if (int e = set_smem(kern, bytes)) return e;
+      hipLaunchKernelGGL(kern, grid, block, bytes, st, p);
+      return 0;
+    };
+    if constexpr (CAN_FOLD)
+      if (p.lsec) return launch(std::true_type{});
+    return launch(std::false_type{});
   };
   auto go = [&](auto SRDV) -> int {
     if constexpr (FUSED) {

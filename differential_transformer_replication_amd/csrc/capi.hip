@@ -295,6 +295,9 @@ int dta_attn_bwd(const dta_attn_bwd_args* a, void* stream) {
   p.rope = a->rope_freqs;
   if (a->dcoef_partial && !aligned_ptr(a->dcoef_partial)) return DTA_ERR_INVALID;
   if (a->dv_f32 && !aligned_ptr(a->dv_f32)) return DTA_ERR_INVALID;
+  if (a->lse_c && !aligned_ptr(a->lse_c)) return DTA_ERR_INVALID;
+  // |c_i| folded into the key-major kernel's probabilities: 16-bit plans without dropout
+  p.lsec = (a->lse_c && a->dtype != DTA_F32 && !p.drop_thr) ? a->lse_c : nullptr;
   p.dcoef_part = a->dcoef_partial;
   p.B = a->B; p.T = a->T; p.H = a->H; p.N = a->n_terms; p.HS = a->head_size; p.DV = a->dv;
   p.scale = a->scale; p.sl2 = a->scale * kLog2e;
@@ -313,6 +316,7 @@ int dta_attn_bwd(const dta_attn_bwd_args* a, void* stream) {
     if (q.dq.p) off(q.dq);
     if (q.dq32) q.dq32 += (int64_t)g0 * p.HS;
     q.lse += g0 * rowvec; q.delta += g0 * rowvec; q.coef += g0; q.dcoef += g0;
+    if (q.lsec) q.lsec += g0 * rowvec;
     if (q.dcoef_part) q.dcoef_part += g0 * (int64_t)p.B * nblk;
     q.N = ng; q.br0 = g0; q.dv_acc = g0 > 0; q.dv_last = g0 + ng == p.N;
     return q;

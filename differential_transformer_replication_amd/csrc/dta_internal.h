@@ -56,6 +56,8 @@ struct BwdParams {
   float* dv32;         // optional fp32 [b][t][h][e] running dV sum across branch groups
   int dv_last;         // the last dK/dV group (with dv32: the one that writes dv)
   int ob16;            // obr holds fp16 O_i (ABI 6)
+  float* lsec;         // optional (ABI 8 lse_c, 16-bit, no dropout): stored LSE_i + log2|c_i| rows
+                       // [i][b][h][t], written by attn_dq, the S seeds of attn_dkdv (|c_i| folded into P)
 };
 
 // per-dtype launchers (dtype index: 0 bf16, 1 f16, 2 f32); return hipError_t

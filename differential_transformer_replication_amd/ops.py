@@ -125,6 +125,10 @@ def _obr_dtype(dtype: torch.dtype) -> torch.dtype:
 # in more than one branch group.  Always on in the product; the C ABI's other path (dv_f32 NULL:
 # each later group adds into the 16-bit dV) is exercised by the GPU tests with it off.
 _DV_F32_WORKSPACE = [True]
+# Whether the backward hands dta_attn_bwd the ABI 8 lse_c workspace (16-bit, no dropout: the key-major
+# kernel folds |c_i| into its probabilities).  Always on in the product; the GPU tests turn it off to
+# run the C ABI's unfolded 16-bit path.
+_LSE_C_WORKSPACE = [True]
 
 # Backward branch-group caps handed to dta_attn_bwd (ABI 7 group_max_dq / group_max_dkdv);
 # (0, 0) = the library's per-stage defaults.  Tests set them with ``bwd_group_caps`` to run
@@ -220,6 +224,9 @@ class _DiffAttention(torch.autograd.Function):
         caps = ctx.caps
         if dt != _lib.DTA_F32 and _DV_F32_WORKSPACE[0] and lib.dta_attn_bwd_dkdv_groups(dt, hs, N, dv, caps[1]) > 1:
             dv32 = torch.empty(B, T, H, dv, device=dev, dtype=torch.float32)
+        # ABI 8: the |c_i|-folded key-major kernel's score seeds (16-bit, no dropout; private workspace)
+        lsec = (torch.empty(N, B, H, T, device=dev, dtype=torch.float32)
+                if dt != _lib.DTA_F32 and ctx.drop[0] == 0.0 and _LSE_C_WORKSPACE[0] else None)
         # with RoPE the kernels differentiate w.r.t. the rotated Q/K (qk_rot) and their
         # dQ / dK epilogues apply the inverse rotation, writing straight into dqkv
         obr_t = _lib.DtaTensor(obr.data_ptr(), *obr.stride()[1:4], obr.stride(0))
@@ -230,7 +237,8 @@ class _DiffAttention(torch.autograd.Function):
                              dcoef.data_ptr(), delta.data_ptr(), None, _lib.BWD_PRE,
                              freqs.data_ptr() if freqs is not None else None, dcp.data_ptr(), ctx.drop[1],
                              _lib.dtype_code(obr.dtype), *caps,
-                             dv32.data_ptr() if dv32 is not None else None)
+                             dv32.data_ptr() if dv32 is not None else None,
+                             lsec.data_ptr() if lsec is not None else None)
         _lib.check(lib.dta_attn_bwd(a, stream))
         a.stages = _lib.BWD_DQ
         with TIMER.region("attn_bwd_dq"):

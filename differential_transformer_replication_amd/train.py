@@ -201,9 +201,12 @@ _BUCKET_CLIP = os.environ.get("DTA_BUCKET_CLIP", "1") != "0"    # A/B switch: 0 
 class Trainer:
     """One optimizer step = grad_acc_steps micro-steps + DP sync + clip + AdamW."""
 
-    def __init__(self, cfg: TrainingConfig, model: torch.nn.Module, world: int, rank: int, device):
+    def __init__(self, cfg: TrainingConfig, model: torch.nn.Module, world: int, rank: int, device,
+                 reduce_single: bool = False):
         self.cfg, self.model, self.world, self.rank = cfg, model, world, rank
-        self.sync = BucketedAllReduce(model, cfg.bucket_cap_mb)
+        # reduce_single: launch every bucket's all-reduce from the backward hooks even in a
+        # 1-rank group (bench.py times the hook / launch overhead an N-rank run carries)
+        self.sync = BucketedAllReduce(model, cfg.bucket_cap_mb, reduce_single=reduce_single)
         self.opt = AdamW(model.parameters(), lr=cfg.learning_rate, betas=(cfg.beta1, cfg.beta2),
                          weight_decay=cfg.weight_decay, fused=device.type == "cuda")
         self.sched = CosineWarmupScheduler(self.opt, cfg.warmup_iters, cfg.max_iters, cfg.min_lr)
@@ -349,7 +352,10 @@ def train_bench(args, world, rank):
     g = torch.Generator(device="cpu").manual_seed(cfg.seed + rank)
     tokens = torch.randint(0, cfg.vocab_size, (4_000_000 if cuda else 100_000,), generator=g).to(dev)
     it = ShardedWindows(tokens, cfg.block_size, cfg.micro_batch_size, rank, world, cfg.seed)
-    tr = Trainer(cfg, model, world, rank, dev)
+    single = bool(getattr(args, "reduce_single", False)) and cuda and world == 1
+    if single and not dist.is_initialized():
+        raise RuntimeError("reduce_single needs an initialised (1-rank) process group")
+    tr = Trainer(cfg, model, world, rank, dev, reduce_single=single)
     for _ in range(args.warmup):
         tr.step(it.next)
     sync()
@@ -377,7 +383,9 @@ def train_bench(args, world, rank):
                       "global_batch": cfg.micro_batch_size * world, "seq_len": cfg.block_size,
                       "parallelism": (f"dp{world} (bucketed {'RCCL' if cuda else 'gloo'} all-reduce, "
                                       f"{cfg.bucket_cap_mb} MB buckets, overlapped with backward)") if world > 1
-                      else "dp1, no collective (one rank: the bucket all-reduces are not launched)"}}
+                      else ("dp1 over a 1-rank RCCL group: every bucket all-reduce launched from the backward "
+                            f"hooks ({cfg.bucket_cap_mb} MB buckets)" if single else
+                            "dp1, no collective (one rank: the bucket all-reduces are not launched)")}}
     if cuda:
         res["model_tflops"] = round(fpt * tps / 1e12, 2)
         res["mfu"] = round(fpt * tps / 1e12 / (world * PEAK_BF16_TFLOPS), 4)

@@ -43,7 +43,8 @@
 extern "C" {
 #endif
 
-#define DTA_ABI_VERSION 7   /* 7: per-stage backward branch-group caps (group_max_dq, group_max_dkdv);
+#define DTA_ABI_VERSION 8   /* 8: lse_c workspace (the key-major kernel folds |c_i| into its probabilities);
+                               7: per-stage backward branch-group caps (group_max_dq, group_max_dkdv);
                                6: obr_dtype (fp16 O_i for 16-bit activations);
                                5: RoPE of Q_i at the forward's load (rope_freqs, q_rot);
                                4: Obr is fp32 for every dtype; any n_terms >= 1 */
@@ -161,6 +162,12 @@ typedef struct dta_attn_bwd_args {
                                 group (dta_attn_bwd_dkdv_groups > 1), the running dV sum stays here
                                 in fp32 and only the last group rounds it to dtype.  NULL: each later
                                 group adds into dv_out (one extra 16-bit rounding per group). */
+  float* lse_c;              /* ABI 8, optional fp32 workspace [i][b][h][t] (n_terms*B*H*T floats, 16-byte
+                                aligned), PRIVATE to the backward like delta: with 16-bit activations and
+                                no dropout the DQ stage writes each row's stored LSE_i + log2|c_i| here and
+                                the DKDV stage seeds its scores with it, so its probabilities come out
+                                already scaled by |c_i| (one VALU op per element less in dV's operand).
+                                Requires |c_i| < 2^64.  NULL (or fp32 / dropout): the unfolded kernels. */
 } dta_attn_bwd_args;
 
 enum { DTA_BWD_PRE = 1, DTA_BWD_DQ = 2, DTA_BWD_DKDV = 4 };

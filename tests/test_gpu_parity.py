@@ -114,6 +114,49 @@ def test_core_dv_groups_without_f32_workspace(dtype, H, N, hs, T, rope):
         ops._DV_F32_WORKSPACE[0] = True
 
 
+# ABI 8 lse_c = NULL: the 16-bit key-major kernel without the |c_i| fold (the C ABI's other path;
+# ops always passes the workspace), including negative and zero first coefficients.
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("H,N,hs,T,rope", [(2, 2, 64, 129, False), (2, 3, 64, 65, True), (1, 2, 128, 130, False)])
+def test_core_without_lse_c(dtype, H, N, hs, T, rope):
+    ops = _ops()
+    ops._LSE_C_WORKSPACE[0] = False
+    try:
+        _core_case(dtype, H, N, hs, T, rope)
+    finally:
+        ops._LSE_C_WORKSPACE[0] = True
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("c0", [-0.7, 0.0])
+def test_core_fold_signs(dtype, c0):
+    """The |c_i| fold (ABI 8 lse_c) with a negative or zero first coefficient and mixed signs:
+    dV's operand is formed relative to branch 0's sign, dK_i takes sign(c_i), c_i = 0 gives P~ = 0."""
+    ops = _ops()
+    H, N, hs, T, B = 3, 3, 64, 150, 2
+    g = torch.Generator().manual_seed(77)
+    W = ops.packed_width(H, N, hs, 2 * hs)
+    qkv = torch.randn(B, T, W, generator=g)
+    coef = torch.tensor([[c0, -0.4, 0.3], [c0, 0.5, -0.2], [1.0, 0.0, -0.6]])
+    do = torch.randn(B, T, H * 2 * hs, generator=g)
+    x64 = qkv.to(dtype).double().requires_grad_(True)
+    c64 = coef.double().clone().requires_grad_(True)
+    ref = _oracle_core(x64, c64, H, N, hs)
+    ref.backward(do.to(dtype).double())
+    xg = qkv.to(dtype).to(DEV).requires_grad_(True)
+    cg = coef.to(DEV).requires_grad_(True)
+    out = ops.diff_attention(xg, cg, H, N, hs)
+    out.backward(do.to(dtype).to(DEV))
+    torch.cuda.synchronize()
+    tol = TOL[dtype]
+    assert rel_err(out.float().cpu(), ref) < tol
+    nq = H * N * hs
+    gx = xg.grad.float().cpu()
+    for name, sl in (("dQ", slice(0, nq)), ("dK", slice(nq, 2 * nq)), ("dV", slice(2 * nq, None))):
+        assert rel_err(gx[..., sl], x64.grad[..., sl]) < tol, name
+    assert rel_err(cg.grad.cpu(), c64.grad) < tol, "dcoef"
+
+
 # ABI 6 obr_dtype = fp16 (ops: DTA_OBR_F16=1, 16-bit activations): O_i stored as fp16 for the
 # backward's delta_i.  The forward's epilogue then keeps its per-lane stores (the LDS bounce
 # takes fp32 O_i only), so this also covers that path; parity against fp64 at the usual bar.

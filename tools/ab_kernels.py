@@ -110,6 +110,10 @@ def main():
                 dv32 = torch.empty(B, T, H, dv, device=dev)
                 ba.dv_f32 = dv32.data_ptr()
                 keep.append(dv32)
+        # ABI 8 lse_c workspace (as ops): builds without it ignore the field
+        lsec = torch.empty(N, B, H, T, device=dev)
+        ba.lse_c = lsec.data_ptr()
+        keep.append(lsec)
         state[name] = (lib, fa, ba, (o, obr, lse, dqkv, dcoef), keep)
 
     def run(name, which):
