@@ -529,6 +529,11 @@ def train_leg(args, world, rank):
     if world == 1 and args.device == "cuda" and args.rccl_world1:
         torch.cuda.empty_cache()
         own = not dist.is_initialized()
+        # RCCL prints a version banner on stdout when the communicator comes up: keep this
+        # process's stdout to the one JSON line (fd 1 -> fd 2 for the leg)
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
         try:
             if own:
                 import socket
@@ -549,6 +554,9 @@ def train_leg(args, world, rank):
         finally:
             if own and dist.is_initialized():
                 dist.destroy_process_group()
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
     return out
 
 

@@ -642,7 +642,7 @@ inline bool kv_layout_ok(const P& p, int es) {
 #define DTA_FWD_TR_EARLY 0       // A/B: the forward's first d-block V^T reads issued before the last softmax
 #endif
 #ifndef DTA_FWD_SEED
-#define DTA_FWD_SEED 0           // A/B: forward Q_i pre-scaled by scale*log2e, S seeded with -m by one MFMA (FAST tiles)
+#define DTA_FWD_SEED 0           // A/B: forward Q_i pre-scaled by scale*log2e, S seeded with -m by one MFMA (FAST tiles): r06e cfg2 fwd 0.874 -> 0.854 ms, but the bf16 Q*scale rounding moved the forward LSE / O_i off the backward kernels and broke the d(coef) / large-logit bars (r06f): off
 #endif
 #ifndef DTA_FWD_FAST
 #define DTA_FWD_FAST 1
@@ -956,8 +956,8 @@ void attn_fwd_kernel(FwdParams p) {
   // SEED (with FAST): Q_i are pre-scaled by scale*log2e once (registers and LDS), so scores come
   // out of QK^T in log2 units, and on the fixed-reference tiles each branch's S accumulators
   // start at -m by one extra MFMA (a ones fragment times the row constant split into hi + lo
-  // halves, as in attn_dq): P = exp2(S) needs no fma.  Every m is kept at a value the two halves
-  // represent exactly, so the first tile, the seeded tiles and the LSE agree.
+  // halves, as in attn_dq): P = exp2(S) needs no fma.  Entering those tiles each m moves to a value
+  // the two halves represent exactly, so the seeded tiles, the earlier ones and the LSE agree.
   constexpr bool FSEED = DTA_FWD_SEED && FAST;
   static_assert(FSEED == FSEED_Q, "FSEED_Q restates FAST's condition");
   typename O::frag f_one = O::zero(), f_nm[FSEED ? N : 1];
@@ -1042,7 +1042,7 @@ void attn_fwd_kernel(FwdParams p) {
     }
     const float mx = wave_max_halves(row_max(sa)) * (FSEED ? 1.f : p.sl2);
     if (__any(mx > m[i] + THR)) {
-      const float mnew = FSEED ? mrep(fmaxf(m[i], mx)) : fmaxf(m[i], mx);
+      const float mnew = fmaxf(m[i], mx);
       const float alpha = exp2_fast(m[i] - mnew);
       m[i] = mnew;
       l[i] *= alpha;
@@ -1284,8 +1284,20 @@ void attn_fwd_kernel(FwdParams p) {
     for (int kt = nfull; kt < kslow; ++kt) step(kt, std::true_type{}, std::false_type{});
     if constexpr (FAST) {
       if constexpr (FSEED) {
+        // the fixed reference moves to the nearest value the seed's two E halves represent (the
+        // first tile's sums and accumulators follow it, a factor of 1 + O(2^-16)); one the halves
+        // cannot hold (fp16 beyond 65504) sends the workgroup to the exact per-tile-maximum re-run
 #pragma unroll
-        for (int i = 0; i < N; ++i) f_nm[i] = seed_frag<E>(-m[i], hf);     // m[i] = hi + lo exactly
+        for (int i = 0; i < N; ++i) {
+          const float mr = mrep(m[i]);
+          if (!(fabsf(mr) < INFINITY)) bad = 1.f;
+          const float a = (fabsf(mr) < INFINITY) ? exp2_fast(m[i] - mr) : 1.f;
+          l[i] *= a;
+#pragma unroll
+          for (int d = 0; d < NDB; ++d) acc[i][d] *= a;
+          m[i] = (fabsf(mr) < INFINITY) ? mr : m[i];
+          f_nm[i] = seed_frag<E>(-m[i], hf);
+        }
       }
       for (int kt = kslow; kt < nfull; ++kt) step(kt, std::false_type{}, std::true_type{});
       for (int kt = max(kslow, nfull); kt < ntiles; ++kt) step(kt, std::true_type{}, std::true_type{});

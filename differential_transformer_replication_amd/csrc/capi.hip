@@ -276,7 +276,8 @@ int dta_attn_bwd(const dta_attn_bwd_args* a, void* stream) {
   if (!a->dcoef) return DTA_ERR_INVALID;
   hipStream_t st = (hipStream_t)stream;
   const int stages = a->stages ? a->stages : (DTA_BWD_PRE | DTA_BWD_DQ | DTA_BWD_DKDV);
-  if (stages & DTA_BWD_PRE) {
+  // (with dcoef_partial the DQ stage's ordered reduce overwrites every dcoef entry: nothing to zero)
+  if ((stages & DTA_BWD_PRE) && !a->dcoef_partial) {
     if (hipMemsetAsync(a->dcoef, 0, sizeof(float) * a->H * a->n_terms, st)) return DTA_ERR_LAUNCH;
   }
   if ((int64_t)a->B * a->T == 0) return DTA_OK;

@@ -239,7 +239,7 @@ class _DiffAttention(torch.autograd.Function):
                              _lib.dtype_code(obr.dtype), *caps,
                              dv32.data_ptr() if dv32 is not None else None,
                              lsec.data_ptr() if lsec is not None else None)
-        _lib.check(lib.dta_attn_bwd(a, stream))
+        # (no PRE stage: with the d(coef) partials the DQ stage's ordered reduce writes dcoef whole)
         a.stages = _lib.BWD_DQ
         with TIMER.region("attn_bwd_dq"):
             _lib.check(lib.dta_attn_bwd(a, stream))

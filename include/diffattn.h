@@ -131,7 +131,8 @@ typedef struct dta_attn_bwd_args {
   float* dcoef;              /* output fp32 [h][i] (overwritten) */
   float* delta;              /* workspace fp32 [i][b][h][t] */
   float* dq_f32;             /* see above */
-  int32_t stages;            /* 0 = all; else bitmask of DTA_BWD_PRE (zero dcoef),
+  int32_t stages;            /* 0 = all; else bitmask of DTA_BWD_PRE (zero dcoef; a no-op when
+                                dcoef_partial is given, whose ordered reduce writes dcoef whole),
                                 DTA_BWD_DQ (query-major kernel), DTA_BWD_DKDV
                                 (key-major kernel) -- lets a caller bracket one
                                 kernel with events on the same stream; DQ must
