@@ -26,8 +26,8 @@ __all__ = ["precompute_freqs_cis", "apply_rotary_emb", "Head", "MultiHeadAttenti
 
 
 def _fused_ok(x: torch.Tensor, p: float, hs: int) -> bool:
-    # the fused kernels' standard-attention plans (dv = hs: head sizes 32, 64, 96, 128, and
-    # every other head size up to 128 zero-padded to one of them, ops.padded_head);
+    # the fused kernels' standard-attention plans (dv = hs: head sizes 32, 64, 96, 128, 256, and
+    # every other head size up to 256 zero-padded to one of them, ops.padded_head);
     # x.dtype is the projection's dtype under autocast too
     dt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else x.dtype
     return x.is_cuda and 0.0 <= p < 1.0 and ops.attention_supported(dt, hs, 1, hs)

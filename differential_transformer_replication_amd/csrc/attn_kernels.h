@@ -756,6 +756,9 @@ struct FwdPick {
 #ifndef DTA_BWD_BOUNCE
 #define DTA_BWD_BOUNCE 1
 #endif
+#ifndef DTA_BOUNCE_NT
+#define DTA_BOUNCE_NT 0          // A/B: bounced whole-row stores non-temporal: 1 the fp32 ones (O_i, dV sums), 2 all
+#endif
 template <class OutT, int NDB, class Val>
 __device__ __forceinline__ void bounce_store(float* reg, int lane, Val&& val, OutT* dst, int64_t ld, int nrows) {
   const int r = lane & 31, hf = lane >> 5;
@@ -777,7 +780,10 @@ __device__ __forceinline__ void bounce_store(float* reg, int lane, Val&& val, Ou
       for (int k = 0; k < 8; ++k) {
         const int rr = k * 4 + (lane >> 4), c = lane & 15;
         const f32x4 v = *reinterpret_cast<const f32x4*>(reg + rr * 64 + ((c ^ (rr & 15)) << 2));
-        if (rr < nrows) *reinterpret_cast<f32x4*>(dst + rr * ld + h * 64 + c * 4) = v;
+        if (rr < nrows) {
+          if constexpr (DTA_BOUNCE_NT >= 1) __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(dst + rr * ld + h * 64 + c * 4));
+          else *reinterpret_cast<f32x4*>(dst + rr * ld + h * 64 + c * 4) = v;
+        }
       }
     } else {
       typedef OutT v8 __attribute__((ext_vector_type(8)));
@@ -787,7 +793,10 @@ __device__ __forceinline__ void bounce_store(float* reg, int lane, Val&& val, Ou
         const f32x4 a = *reinterpret_cast<const f32x4*>(reg + rr * 64 + ((c ^ (rr & 15)) << 2));
         const f32x4 bq = *reinterpret_cast<const f32x4*>(reg + rr * 64 + (((c + 1) ^ (rr & 15)) << 2));
         const v8 v = {(OutT)a[0], (OutT)a[1], (OutT)a[2], (OutT)a[3], (OutT)bq[0], (OutT)bq[1], (OutT)bq[2], (OutT)bq[3]};
-        if (rr < nrows) *reinterpret_cast<v8*>(dst + rr * ld + h * 64 + c * 4) = v;
+        if (rr < nrows) {
+          if constexpr (DTA_BOUNCE_NT >= 2) __builtin_nontemporal_store(v, reinterpret_cast<v8*>(dst + rr * ld + h * 64 + c * 4));
+          else *reinterpret_cast<v8*>(dst + rr * ld + h * 64 + c * 4) = v;
+        }
       }
     }
     __builtin_amdgcn_wave_barrier();
@@ -1562,7 +1571,7 @@ void attn_dq_kernel(BwdParams p) {
   // plans that spill (16-bit head size 128 at N >= 3: 84-508 B/lane of scratch; dropout
   // plans: up to 532 B/lane) read LDS only through compiler-tracked loads: no asm read
   // whose destination the allocator could spill before it lands (see tr_load)
-  constexpr bool SPILLS = sizeof(E) == 2 && (DROP || (HS >= 128 && N >= 3));
+  constexpr bool SPILLS = sizeof(E) == 2 && (DROP || (HS >= 128 && N >= 3) || (HS >= 192 && N >= 2));
   // DTA_DQ_EARLY_RING: the ring's first stages are issued before the per-row loads and the
   // delta_i reduction below, so their DMA overlaps the O_i reads instead of following them
   constexpr bool EARLY = DTA_DQ_EARLY_RING && SRD;
@@ -2118,7 +2127,7 @@ void attn_dkdv_kernel(BwdParams p) {
   constexpr int NHB = (HS + 31) / 32, NVB = DV / 32;
   // the plans that spill (16-bit head size 128 at N >= 3, the dropout plans: 8-48 VGPRs at
   // head size 64 N = 2) take compiler-tracked transposed reads (see tr_load)
-  constexpr bool SPILLS = sizeof(E) == 2 && (DROP || (HS >= 128 && N >= 3));
+  constexpr bool SPILLS = sizeof(E) == 2 && (DROP || (HS >= 128 && N >= 3) || (HS >= 192 && N >= 2));
 
   using KI = Img<E, KP>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -2816,6 +2825,11 @@ int launch_dkdv_t(const BwdParams& p, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
+// Head size 256 (16-bit diff plans; fp32 only the control's dv = hs one fits): head sizes 129-256
+// run there zero-padded (ops.padded_head), the reference accepting any n_embd // (2 n_head)
+// (diff_transformer.py:111).  Its N = 2 backward plans spill, so the backward runs it as
+// single-branch groups (capi.hip bwd_group_cap) and those plans read LDS through
+// compiler-tracked loads (SPILLS).
 // (head size, branches, value width): the differential models' dv = 2 hs, plus the
 // control model's standard attention (N = 1, dv = hs; control.py:38-63).  Head size 96
 // is the reference's own TrainingConfig (n_embd 768, n_head 4: train.py:60-61 with
@@ -2826,7 +2840,8 @@ int launch_dkdv_t(const BwdParams& p, hipStream_t st) {
   X(16, 1, 32) X(16, 2, 32) X(16, 3, 32) X(16, 4, 32) X(32, 1, 64) X(32, 2, 64) X(32, 3, 64) X(32, 4, 64) \
   X(64, 1, 128) X(64, 2, 128) X(64, 3, 128) X(64, 4, 128) X(128, 1, 256) X(128, 2, 256) X(128, 3, 256) \
   X(128, 4, 256) X(64, 1, 64) X(128, 1, 128) X(32, 1, 32) \
-  X(96, 1, 192) X(96, 2, 192) X(96, 3, 192) X(96, 4, 192) X(96, 1, 96)
+  X(96, 1, 192) X(96, 2, 192) X(96, 3, 192) X(96, 4, 192) X(96, 1, 96) \
+  X(256, 1, 512) X(256, 2, 512) X(256, 1, 256)
 #endif
 
 // whether the N-branch plan of (HS, N, DV) is built for E

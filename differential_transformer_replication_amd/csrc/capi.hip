@@ -106,6 +106,7 @@ int bwd_group_cap(int dtype, int hs, int n, bool dkdv) {
   return DTA_BWD_GROUP_MAX;
 #else
   if (dtype == DTA_F32) return 4;
+  if (hs >= 192) return 1;            // head size 256: the single-branch plans (the N = 2 ones spill)
   if (dkdv) return hs >= 64 ? 2 : 4;
   return (hs >= 128 || (hs >= 64 && hs < 96 && n >= 4)) ? 2 : 4;
 #endif

@@ -82,10 +82,11 @@ def padded_head(dtype: torch.dtype, hs: int, N: int, dv: int) -> Optional[int]:
     built, else the smallest built head size above it (Q_i / K_i and V zero-padded, see
     ``diff_attention``), else None.  The reference accepts any head size
     (head_size = n_embd // (2 n_head), diff_transformer.py:111); the plans are built for
-    16, 32, 64, 96 and 128."""
+    16, 32, 64, 96, 128 and 256 (256: 16-bit diff plans, and the control's dv = hs in every
+    dtype)."""
     if N < 1 or hs < 1 or dv not in (hs, 2 * hs) or (dv == hs and N != 1):
         return None
-    for hp in (hs,) + tuple(h for h in (16, 32, 64, 96, 128) if h > hs):
+    for hp in (hs,) + tuple(h for h in (16, 32, 64, 96, 128, 256) if h > hs):
         if supported(dtype, hp, N, hp if dv == hs else 2 * hp):
             return hp
     return None
@@ -274,7 +275,7 @@ def diff_attention(qkv: Tensor, coef: Tensor, H: int, N: int, hs: int,
     hp = padded_head(qkv.dtype, hs, N, dv) if qkv.is_cuda else hs
     if hp is None:
         raise RuntimeError(f"no gfx950 kernel for head_size={hs}, n_terms={N}, dv={dv}, dtype={qkv.dtype} "
-                           "(head sizes up to 128 are served)")
+                           "(head sizes up to 256 are served; 129-256 in 16-bit for the differential models)")
     if hp == hs:
         return _DiffAttention.apply(qkv, coef, H, N, hs, freqs, dv, dropout_p, int(seed), scale)
     # a head size without its own plan runs in the next built one: Q_i / K_i zero-padded

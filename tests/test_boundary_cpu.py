@@ -56,7 +56,11 @@ def test_padded_head_sizes_without_gpu():
     assert ops.padded_head(torch.bfloat16, 100, 3, 200) == 128
     assert ops.padded_head(torch.bfloat16, 80, 1, 80) == 96
     assert ops.padded_head(torch.bfloat16, 16, 1, 16) == 32
-    assert ops.padded_head(torch.bfloat16, 136, 2, 272) is None
+    assert ops.padded_head(torch.bfloat16, 136, 2, 272) == 256      # 129-256: the 16-bit head-size-256 plans
+    assert ops.padded_head(torch.float16, 256, 3, 512) == 256
+    assert ops.padded_head(torch.float32, 136, 2, 272) is None          # fp32 diff plans stop at 128
+    assert ops.padded_head(torch.float32, 200, 1, 200) == 256           # the control's dv = hs plan
+    assert ops.padded_head(torch.bfloat16, 264, 2, 528) is None
     assert ops.padded_head(torch.bfloat16, 64, 2, 64) is None        # dv = hs only for N = 1
 
 

@@ -8,9 +8,9 @@ runs fp32 with no autocast (train.py:124-138).  Here:
   runs as branch groups that have one (csrc/capi.hip): the forward as N single-branch
   workgroups plus a run-time-N combine, the backward group by group, dV summed over the
   groups, d(coef) reduced over all N;
-- a head size without its own plan (up to 128) runs zero-padded in the next built one
-  (ops.padded_head): zero Q_i / K_i columns leave every score unchanged, zero V columns
-  add output columns that are dropped.
+- a head size without its own plan (up to 128; 129-256 in 16-bit on the head-size-256 plans)
+  runs zero-padded in the next built one (ops.padded_head): zero Q_i / K_i columns leave every
+  score unchanged, zero V columns add output columns that are dropped.
 
 Checked against the fp64 oracle at the north star's tolerances (fp32 1e-4, bf16 2e-2).
 """
@@ -115,11 +115,16 @@ def test_padded_head_sizes(dtype, H, N, hs, T, rope, std):
     _core_case(dtype, H, N, hs, T, rope, dv=dv)
 
 
-def test_head_size_above_128_raises():
+def test_head_size_limits_raise():
+    """Head sizes 129-256 run in 16-bit on the head-size-256 plans (test_gpu_parity.py
+    test_core_large_head_sizes); fp32 differential plans stop at 128 and nothing goes past 256."""
     ops = _ops()
     x = torch.zeros(1, 4, ops.packed_width(1, 2, 136, 272), device=DEV)
     with pytest.raises(RuntimeError, match="no gfx950 kernel"):
         ops.diff_attention(x, torch.ones(1, 2, device=DEV), 1, 2, 136)
+    x = torch.zeros(1, 4, ops.packed_width(1, 2, 264, 528), device=DEV, dtype=torch.bfloat16)
+    with pytest.raises(RuntimeError, match="no gfx950 kernel"):
+        ops.diff_attention(x, torch.ones(1, 2, device=DEV), 1, 2, 264)
 
 
 def _oracle_alternating_transformer(sd, idx, tgt, n_head, n_layer, n_terms, block):

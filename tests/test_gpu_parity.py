@@ -114,6 +114,47 @@ def test_core_dv_groups_without_f32_workspace(dtype, H, N, hs, T, rope):
         ops._DV_F32_WORKSPACE[0] = True
 
 
+# Head sizes above 128 (the reference takes any n_embd // (2 n_head), diff_transformer.py:111): the
+# 16-bit head-size-256 plans, directly and zero-padded (160), N = 1..3 (the backward as single-branch
+# groups), RoPE on some.
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("H,N,hs,T,rope", [(1, 2, 256, 70, False), (2, 1, 256, 97, True), (1, 3, 256, 65, True),
+                                           (2, 2, 160, 130, True), (1, 2, 200, 40, False)])
+def test_core_large_head_sizes(dtype, H, N, hs, T, rope):
+    assert _ops().padded_head(dtype, hs, N, 2 * hs) == 256
+    _core_case_any(dtype, H, N, hs, T, rope)
+
+
+def _core_case_any(dtype, H, N, hs, T, rope):
+    """_core_case through ops.diff_attention's padding (head sizes without their own plan)."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(1000 * H + 100 * N + hs + T)
+    B = 2
+    W = ops.packed_width(H, N, hs, 2 * hs)
+    qkv = torch.randn(B, T, W, generator=g)
+    coef = torch.randn(H, N, generator=g) * 0.5
+    coef[:, 0] = 1.0
+    do = torch.randn(B, T, H * 2 * hs, generator=g)
+    freqs_c = orc.precompute_freqs_cis(hs, max(T, 8)) if rope else None
+    x64 = qkv.to(dtype).double().requires_grad_(True)
+    c64 = coef.double().clone().requires_grad_(True)
+    ref = _oracle_core(x64, c64, H, N, hs, freqs_c)
+    ref.backward(do.to(dtype).double())
+    xg = qkv.to(dtype).to(DEV).requires_grad_(True)
+    cg = coef.to(DEV).requires_grad_(True)
+    freqs = torch.view_as_real(freqs_c[:T]).contiguous().to(DEV) if rope else None
+    out = ops.diff_attention(xg, cg, H, N, hs, freqs)
+    out.backward(do.to(dtype).to(DEV))
+    torch.cuda.synchronize()
+    tol = TOL[dtype]
+    assert rel_err(out.float().cpu(), ref) < tol
+    nq = H * N * hs
+    gx = xg.grad.float().cpu()
+    for name, sl in (("dQ", slice(0, nq)), ("dK", slice(nq, 2 * nq)), ("dV", slice(2 * nq, None))):
+        assert rel_err(gx[..., sl], x64.grad[..., sl]) < tol, name
+    assert rel_err(cg.grad.cpu(), c64.grad) < tol, "dcoef"
+
+
 # ABI 8 lse_c = NULL: the 16-bit key-major kernel without the |c_i| fold (the C ABI's other path;
 # ops always passes the workspace), including negative and zero first coefficients.
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
