@@ -756,8 +756,15 @@ struct FwdPick {
 #ifndef DTA_BWD_BOUNCE
 #define DTA_BWD_BOUNCE 1
 #endif
+// Non-temporal bounced stores (whole 256-byte row segments, unlike the per-lane 16-byte stores
+// that measured much slower NT in round 4): 1 = the fp32 ones -- the forward's O_i (537 MB at
+// cfg2, read back once by attn_dq) and the dV sums -- so they stop evicting the operands the next
+// kernels read from the Infinity Cache; 2 = every bounced store.  Step-interleaved A/B
+// (profiles/r06i_ab_bounce_nt.json): cfg2 fwd + dq + dK/dV 2.879 -> 2.838 ms (1) / 2.835 (2),
+// cfg3 N = 3 1.049 -> 1.034 / 1.037.  1 by default: the bf16 outputs (O, dQ, dK, dV) feed the
+// very next kernels of a training step (GroupLN, the projection GEMMs).
 #ifndef DTA_BOUNCE_NT
-#define DTA_BOUNCE_NT 0          // A/B: bounced whole-row stores non-temporal: 1 the fp32 ones (O_i, dV sums), 2 all
+#define DTA_BOUNCE_NT 1
 #endif
 template <class OutT, int NDB, class Val>
 __device__ __forceinline__ void bounce_store(float* reg, int lane, Val&& val, OutT* dst, int64_t ld, int nrows) {

@@ -245,8 +245,12 @@ __device__ __forceinline__ void load_ob8(const void* base, int64_t off, bool h, 
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = (float)v[j];
   } else {
-    const f32x4 a = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(base) + off);
-    const f32x4 b = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(base) + off + 4);
+#ifndef DTA_OBR_LOAD_NT
+#define DTA_OBR_LOAD_NT 0      // A/B: attn_dq's reads of the fp32 O_i (read once) non-temporal
+#endif
+    const f32x4* pa = reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(base) + off);
+    const f32x4 a = DTA_OBR_LOAD_NT ? __builtin_nontemporal_load(pa) : *pa;
+    const f32x4 b = DTA_OBR_LOAD_NT ? __builtin_nontemporal_load(pa + 1) : pa[1];
 #pragma unroll
     for (int j = 0; j < 4; ++j) { o[j] = a[j]; o[4 + j] = b[j]; }
   }
