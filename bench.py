@@ -388,7 +388,9 @@ def configs_leg(args):
             raise RuntimeError(f"cfg3 n_terms={n} leg failed: {proc.stderr[-2000:]}")
         r = json.loads(proc.stdout.strip().splitlines()[-1])
         torch.cuda.empty_cache()
-        sec, flop, kernels = core_run(16, 6, 64, n, 2048, args.cfg_steps, 5)   # warm after the training leg's idle host time
+        # warm after the training leg's idle host time: the step is ~1.1 ms, so 30 warm-up steps
+        # (~35 ms) before 30 timed ones (a 10-step sample after 5 read 5-10% slow, r06l vs r06z probe)
+        sec, flop, kernels = core_run(16, 6, 64, n, 2048, max(args.cfg_steps, 30), 30)
         out[f"cfg3_n{n}"] = {"train_tokens_per_s": r["value"], "train_ms_per_step": r["ms_per_step"],
                              "mfu": r.get("mfu"), "params": r["config"]["params"],
                              "core": {"shape": "B=16 H=6 hs=64 dv=128 T=2048 bf16 causal", "ms_per_step": round(
