@@ -373,6 +373,7 @@ static int ln_common(const dta_ln_args* a, bool bwd) {
   if (fused && a->io_dtype == 0) return DTA_ERR_UNSUPPORTED;
   if (!bwd && fused && (!aligned_ptr(a->res) || !aligned_ptr(a->xo) || a->res_stride % v || a->xo_stride % v))
     return DTA_ERR_INVALID;
+  if (bwd && a->partial && !aligned_ptr(a->partial)) return DTA_ERR_INVALID;   // 16-byte partial rows
   if (bwd && a->dres && (!aligned_ptr(a->dres) || a->dres_stride % v)) return DTA_ERR_INVALID;
   if (bwd && a->dx16 && (!aligned_ptr(a->dx16) || a->dx16_stride % v)) return DTA_ERR_INVALID;
   return DTA_OK;

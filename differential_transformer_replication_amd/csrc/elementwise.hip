@@ -461,6 +461,58 @@ __global__ __launch_bounds__(256) void ln_bwd_reduce2_kernel(const float* part2,
   const int64_t col = e % C;
   (e >= C ? db : dw)[col] += s;
 }
+// The two passes above in ONE launch: a workgroup owns 4*QD consecutive entries of the
+// [2][C] partial row (QD lanes x 4 floats) and one thread row per chunk of blocks
+// (256 / QD chunks), each summing its run of blocks with 16-byte loads; the chunk sums
+// meet in LDS and 4*QD threads add them in chunk order -- a fixed order, so dw / db stay
+// bitwise reproducible (QD = 8: the same order as reduce1 + reduce2, bitwise equal to
+// them).  Saves the second launch, its gap and the part2 round trip (C' is a multiple of
+// 8: quads never straddle dw / db).
+#ifndef DTA_LN_REDUCE_QD
+#define DTA_LN_REDUCE_QD 8
+#endif
+template <int QD>
+__global__ __launch_bounds__(256) void ln_bwd_reduce_kernel(const float* part, int nblk, int64_t C, float* dw, float* db) {
+  constexpr int NCH = 256 / QD, W = 4 * QD;
+  const int t = threadIdx.x, q = t % QD, j = t / QD;
+  const int64_t e0 = (int64_t)blockIdx.x * W + q * 4;
+  const int per = (nblk + NCH - 1) / NCH;
+  const int b0 = j * per, b1 = min(nblk, b0 + per);
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  if (e0 < 2 * C) {
+#pragma unroll 16
+    for (int b = b0; b < b1; ++b) s += *reinterpret_cast<const f32x4*>(part + (int64_t)b * 2 * C + e0);
+  }
+  __shared__ float red[NCH][W + 1];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) red[j][q * 4 + k] = s[k];
+  __syncthreads();
+  if (t < W) {
+    const int64_t e = (int64_t)blockIdx.x * W + t;
+    if (e < 2 * C) {
+      float r = 0.f;
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) r += red[c][t];
+      const int64_t col = e % C;
+      (e >= C ? db : dw)[col] += r;
+    }
+  }
+}
+#ifndef DTA_LN_REDUCE_ONE
+#define DTA_LN_REDUCE_ONE 1      // the one-launch ordered reduce (0: reduce1 + reduce2)
+#endif
+static void ln_bwd_reduce(const LnParams& p, int nblk, hipStream_t st) {
+  if (DTA_LN_REDUCE_ONE) {
+    constexpr int W = 4 * DTA_LN_REDUCE_QD;
+    hipLaunchKernelGGL(ln_bwd_reduce_kernel<DTA_LN_REDUCE_QD>, dim3((unsigned)((2 * p.C + W - 1) / W)), dim3(256), 0, st,
+                       p.partial, nblk, p.C, p.dw, p.db);
+  } else {
+    float* part2 = p.partial + (int64_t)nblk * 2 * p.C;
+    const unsigned g = (unsigned)((2 * p.C + 255) / 256);
+    hipLaunchKernelGGL(ln_bwd_reduce1_kernel, dim3(g, kLnChunks), dim3(256), 0, st, p.partial, nblk, p.C, part2);
+    hipLaunchKernelGGL(ln_bwd_reduce2_kernel, dim3(g), dim3(256), 0, st, part2, p.C, p.dw, p.db);
+  }
+}
 
 
 struct RopeDiv { FastDiv row, T, per_row, N; uint32_t rowlen; };
@@ -539,12 +591,7 @@ int ln_launch(const LnParams& p, bool bwd, hipStream_t st) {
         hipLaunchKernelGGL((ln_bwd_rb_kernel<E, (CH_ + 3) / 4>), dim3(bwd_grid), dim3(256), 0, st, p); \
       else                                                                             \
         hipLaunchKernelGGL((ln_bwd_kernel<E, CH_>), dim3(bwd_grid), dim3(256), 0, st, p); \
-      if (p.partial) {                                                                 \
-        float* part2 = p.partial + (int64_t)bwd_grid * 2 * p.C;                        \
-        const unsigned g = (unsigned)((2 * p.C + 255) / 256);                          \
-        hipLaunchKernelGGL(ln_bwd_reduce1_kernel, dim3(g, kLnChunks), dim3(256), 0, st, p.partial, bwd_grid, p.C, part2); \
-        hipLaunchKernelGGL(ln_bwd_reduce2_kernel, dim3(g), dim3(256), 0, st, part2, p.C, p.dw, p.db); \
-      }                                                                                \
+      if (p.partial) ln_bwd_reduce(p, bwd_grid, st);                                   \
     } else {                                                                           \
       hipLaunchKernelGGL((ln_fwd_kernel<E, CH_>), dim3(fwd_grid), dim3(256), 0, st, p); \
     }                                                                                  \
@@ -565,12 +612,7 @@ int ln_launch_mixed(const LnParams& p, bool bwd, hipStream_t st) {
   if (ch <= CH_) {                                                                               \
     if (bwd) {                                                                                   \
       hipLaunchKernelGGL((ln_bwd_rb_kernel<float, (CH_ + 3) / 4, Y>), dim3(bwd_grid), dim3(256), 0, st, p); \
-      if (p.partial) {                                                                           \
-        float* part2 = p.partial + (int64_t)bwd_grid * 2 * p.C;                                  \
-        const unsigned g = (unsigned)((2 * p.C + 255) / 256);                                    \
-        hipLaunchKernelGGL(ln_bwd_reduce1_kernel, dim3(g, kLnChunks), dim3(256), 0, st, p.partial, bwd_grid, p.C, part2); \
-        hipLaunchKernelGGL(ln_bwd_reduce2_kernel, dim3(g), dim3(256), 0, st, part2, p.C, p.dw, p.db); \
-      }                                                                                          \
+      if (p.partial) ln_bwd_reduce(p, bwd_grid, st);                                             \
     } else {                                                                                     \
       hipLaunchKernelGGL((ln_fwd_kernel<float, CH_, Y>), dim3(fwd_grid), dim3(256), 0, st, p);  \
     }                                                                                            \

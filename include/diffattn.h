@@ -201,7 +201,8 @@ typedef struct dta_ln_args {
   float* dw; float* db;              /* fp32 [C], accumulated (caller zeroes) */
   float* partial;                    /* optional fp32 workspace (dta_ln_bwd_workspace_bytes):
                                         per-block column partials summed in a fixed order, so
-                                        dw/db are bitwise reproducible; NULL: float atomics */
+                                        dw/db are bitwise reproducible; 16-byte aligned;
+                                        NULL: float atomics */
   int32_t io_dtype;                  /* 0: y / dy have `dtype`; else 1 + the y / dy dtype code,
                                         with dtype = DTA_F32 and y / dy DTA_BF16 or DTA_F16 (an fp32
                                         residual stream normalised straight into the autocast

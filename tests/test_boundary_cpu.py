@@ -277,3 +277,17 @@ def test_ln_io_dtype_rules_without_gpu():
     assert lib.dta_ln_fwd(a, None) == -2
     a.io_dtype = 1 + _lib.DTA_BF16
     assert lib.dta_ln_fwd(a, None) == -1            # valid combination, null pointers
+
+
+def test_ln_bwd_partial_alignment_without_gpu():
+    """dta_ln_args.partial holds 16-byte rows (the ordered reduce's vector loads): a
+    misaligned workspace is rejected before any launch; dw / db sizes are unchanged."""
+    lib = _lib.load()
+    fake = 1 << 20                                   # never dereferenced: rejected first
+    a = _lib.LnArgs()
+    a.dtype, a.rows, a.C = _lib.DTA_BF16, 4, 64
+    a.x, a.x_stride, a.w, a.mean, a.rstd = fake, 64, fake, fake, fake
+    a.dy, a.dy_stride, a.dx, a.dx_stride, a.dw, a.db = fake, 64, fake, 64, fake, fake
+    a.partial = fake + 4
+    assert lib.dta_ln_bwd(a, None) == -1
+    assert lib.dta_ln_bwd_workspace_bytes(4096, 2048) >= 2 * 2048 * 4 * 512

@@ -1,6 +1,6 @@
 """One-process A/B of libdiffattn builds on the LayerNorm kernels at the cfg2
 GroupLayerNorm shape (32768 rows x 2048, bf16): dta_ln_fwd and dta_ln_bwd (with the
-ordered dw/db reduce), HIP events, rounds interleaved; dx compared with the first build.
+ordered dw/db reduce), HIP events, rounds interleaved; dx, y and dw/db compared with the first build.
     python tools/ab_ln.py base=lib/libdiffattn_x.so new=lib/libdiffattn.so"""
 import ctypes
 import json
@@ -64,12 +64,16 @@ def main():
                 torch.cuda.synchronize()
                 times[n][kind].append(e0.elapsed_time(e1) / 10 * 1e3)
             if rnd == 0:
+                dw.zero_(); db.zero_()              # one backward from zero: dw / db comparable
+                lib.dta_ln_bwd(ba, stream)
+                torch.cuda.synchronize()
                 if ref is None:
-                    ref = (dx.clone(), y.clone(), rdst.clone())
+                    ref = (dx.clone(), y.clone(), rdst.clone(), dw.clone(), db.clone())
                 else:
                     times[n]["dx_equal"] = bool(torch.equal(ref[0], dx))
                     times[n]["y_equal"] = bool(torch.equal(ref[1], y))
                     times[n]["rope_equal"] = bool(torch.equal(ref[2], rdst))
+                    times[n]["dw_db_equal"] = bool(torch.equal(ref[3], dw) and torch.equal(ref[4], db))
     out = {}
     for n, d in times.items():
         out[n] = {k: (sorted(v)[len(v) // 2] if isinstance(v, list) else v) for k, v in d.items()}
