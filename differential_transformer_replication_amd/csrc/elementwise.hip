@@ -272,14 +272,22 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnParams p) {
 // waves split the row's columns (thread t owns 8-column chunks t, t+256, ...), so a
 // thread's dw/db column partials are only 16*CHB registers and need no cross-wave
 // reduction; the row sums (sum g, sum g*xhat) cross waves through a parity-double-
-// buffered LDS slot, one barrier per row.  The next row's x / dy are loaded before
-// the current row's math.  ~60 VGPRs: 4 workgroups (16 waves) per CU, where the
-// wave-per-row kernel above holds 222 registers for C = 2048 (8 waves per CU).
+// buffered LDS slot, one barrier per row.  The x / dy of the rows PD groups ahead are
+// loaded before the current row's math (a register ring of PD + 1 rows): with 512
+// workgroups (2 per CU, capped so the column partials stay small) one row ahead left
+// ~16 KB in flight per CU; three rows ahead took cfg2's ln_bwd 72.6 -> 68.5 us
+// (profiles/r06o_ab_ln_prefetch_depth.json).  ~114 VGPRs at C = 2048, where the
+// wave-per-row kernel above holds 222.
 #ifndef DTA_LN_BWD_RPI
 #define DTA_LN_BWD_RPI 1         // rows per barrier (each workgroup step)
 #endif
-template <class E, int CHB, class Y = E, int RPI = DTA_LN_BWD_RPI>
+#ifndef DTA_LN_BWD_PD
+#define DTA_LN_BWD_PD 3          // row groups in flight ahead of the one being computed (1..5)
+#endif
+template <class E, int CHB, class Y = E, int RPI = DTA_LN_BWD_RPI, int PD = DTA_LN_BWD_PD>
 __global__ __launch_bounds__(256) void ln_bwd_rb_kernel(LnParams p) {
+  static_assert(PD >= 1 && PD <= 5, "prefetch depth");
+  constexpr int NSL = PD + 1;      // register slots of raw rows
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   float dwp[CHB][8], dbp[CHB][8];
 #pragma unroll
@@ -293,9 +301,9 @@ __global__ __launch_bounds__(256) void ln_bwd_rb_kernel(LnParams p) {
   typedef typename std::conditional<P16, s16x8, f32x4>::type RT;
   typedef typename std::conditional<Y16, s16x8, f32x4>::type RY;
   constexpr int NR = P16 ? 1 : 2, NY = Y16 ? 1 : 2;
-  RT xr[2][RPI][CHB][NR];
-  RY dr[2][RPI][CHB][NY];
-  float mr[2][RPI], rr[2][RPI];
+  RT xr[NSL][RPI][CHB][NR];
+  RY dr[NSL][RPI][CHB][NY];
+  float mr[NSL][RPI], rr[NSL][RPI];
   const int64_t stride = gridDim.x;
   // rows r0 + q*stride, q < RPI; past the last row the last row is re-read (masked in the
   // math): a load behind a branch would leave the wait counters unknown at the join
@@ -347,7 +355,8 @@ __global__ __launch_bounds__(256) void ln_bwd_rb_kernel(LnParams p) {
   }
   auto body = [&](auto S, int64_t r0) {
     constexpr int s = decltype(S)::value;
-    if (r0 + RPI * stride < p.rows) load(std::integral_constant<int, 1 - s>{}, r0 + RPI * stride);   // next rows in flight
+    if (r0 + PD * RPI * stride < p.rows)                       // the rows PD groups ahead in flight
+      load(std::integral_constant<int, (s + PD) % NSL>{}, r0 + PD * RPI * stride);
     float xh[RPI][CHB][8], g[RPI][CHB][8];
 #pragma unroll
     for (int q = 0; q < RPI; ++q) {
@@ -410,12 +419,23 @@ __global__ __launch_bounds__(256) void ln_bwd_rb_kernel(LnParams p) {
   };
   int64_t r = blockIdx.x;
   if (r < p.rows) load(std::integral_constant<int, 0>{}, r);
+  if constexpr (PD >= 2) if (r + RPI * stride < p.rows) load(std::integral_constant<int, 1>{}, r + RPI * stride);
+  if constexpr (PD >= 3) if (r + 2 * RPI * stride < p.rows) load(std::integral_constant<int, 2>{}, r + 2 * RPI * stride);
+  if constexpr (PD >= 4) if (r + 3 * RPI * stride < p.rows) load(std::integral_constant<int, 3>{}, r + 3 * RPI * stride);
+  if constexpr (PD >= 5) if (r + 4 * RPI * stride < p.rows) load(std::integral_constant<int, 4>{}, r + 4 * RPI * stride);
+  // slot s of the ring serves row groups s, s + NSL, ...: the loop unrolled NSL times
+  auto run = [&](auto S) -> bool {
+    body(S, r);
+    r += RPI * stride;
+    return r < p.rows;
+  };
   while (r < p.rows) {
-    body(std::integral_constant<int, 0>{}, r);
-    r += RPI * stride;
-    if (r >= p.rows) break;
-    body(std::integral_constant<int, 1>{}, r);
-    r += RPI * stride;
+    if (!run(std::integral_constant<int, 0>{})) break;
+    if (!run(std::integral_constant<int, 1>{})) break;
+    if constexpr (NSL > 2) if (!run(std::integral_constant<int, 2 % NSL>{})) break;
+    if constexpr (NSL > 3) if (!run(std::integral_constant<int, 3 % NSL>{})) break;
+    if constexpr (NSL > 4) if (!run(std::integral_constant<int, 4 % NSL>{})) break;
+    if constexpr (NSL > 5) if (!run(std::integral_constant<int, 5 % NSL>{})) break;
   }
 #pragma unroll
   for (int c = 0; c < CHB; ++c) {
