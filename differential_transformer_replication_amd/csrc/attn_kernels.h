@@ -644,6 +644,9 @@ inline bool kv_layout_ok(const P& p, int es) {
 #ifndef DTA_FWD_SEED
 #define DTA_FWD_SEED 0           // A/B: forward Q_i pre-scaled by scale*log2e, S seeded with -m by one MFMA (FAST tiles): r06e cfg2 fwd 0.874 -> 0.854 ms, but the bf16 Q*scale rounding moved the forward LSE / O_i off the backward kernels and broke the d(coef) / large-logit bars (r06f): off
 #endif
+#ifndef DTA_FWD_PK
+#define DTA_FWD_PK 0             // A/B: the forward's exp arguments and row sums as packed fp32 pairs (v_pk_*): 161 -> 102 VALU issues, fwd +0.3..0.7% (r06p2): off
+#endif
 #ifndef DTA_FWD_FAST
 #define DTA_FWD_FAST 1
 #endif
@@ -1012,6 +1015,25 @@ void attn_fwd_kernel(FwdParams p) {
     float ls0 = 0.f, ls1 = 0.f;
     // FSEED: scores already in log2 units (seeded tiles: already minus m)
     auto arg = [&](float v) { return FSEED ? (seeded ? v : v - mi) : fmaf(v, p.sl2, -mi); };
+    if constexpr (DTA_FWD_PK && !FSEED) {
+      // the argument fmas and the two row-sum chains as packed pairs (v_pk_fma_f32 /
+      // v_pk_add_f32): element for element the scalar form's arithmetic, bitwise equal
+      f32x2 ls2 = f32x2{0.f, 0.f};
+      const f32x2 sl2v = f32x2{p.sl2, p.sl2}, nmv = f32x2{-mi, -mi};
+#pragma unroll
+      for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+          const f32x2 a2 = __builtin_elementwise_fma(f32x2{sa[kb][r], sa[kb][r + 1]}, sl2v, nmv);
+          const float e0 = exp2_fast(a2[0]);
+          const float e1 = exp2_fast(a2[1]);
+          sa[kb][r] = e0;
+          sa[kb][r + 1] = e1;
+          ls2 += f32x2{e0, e1};
+        }
+      ls0 = ls2[0];
+      ls1 = ls2[1];
+    } else {
 #pragma unroll
     for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
@@ -1023,6 +1045,7 @@ void attn_fwd_kernel(FwdParams p) {
         ls0 += e0;
         ls1 += e1;
       }
+    }
     const float ls = ls0 + ls1;
     l[i] += ls;
     if constexpr (DROP) {
@@ -1478,6 +1501,12 @@ struct DqCfg {
 #ifndef DTA_DKDV_TR_EARLY
 #define DTA_DKDV_TR_EARLY 0      // A/B: dK/dV's transposed Q_i reads issued before the softmax VALU
 #endif
+#ifndef DTA_DQ_PK
+#define DTA_DQ_PK 0              // A/B: dQ's dS math as packed fp32 pairs (v_pk_*): 120 -> 78 VALU issues per step, dq +1% (r06p): off
+#endif
+#ifndef DTA_DKDV_PK
+#define DTA_DKDV_PK 0            // A/B: dK/dV's dS / dV-operand math as packed fp32 pairs (v_pk_*): 123 -> 101 VALU issues, dK/dV +2.8% (r06p): off
+#endif
 #ifndef DTA_DKDV_CFOLD
 #define DTA_DKDV_CFOLD 1         // 0: never build the |c_i|-folded dK/dV instantiations (lse_c ignored)
 #endif
@@ -1843,10 +1872,22 @@ void attn_dq_kernel(BwdParams p) {
                   if constexpr (MASK) arg = (kb * 32 + (r & 3) + 8 * (r >> 2) > lim) ? -INFINITY : arg;
                   pr[u] = exp2_fast(arg);
                 }
+                if constexpr (DTA_DQ_PK && DTA_DQ_EXPG % 2 == 0) {
+                  // two rows per v_pk_mul_f32 / v_pk_add_f32 (same fp32 arithmetic per element)
 #pragma unroll
-                for (int u = 0; u < DTA_DQ_EXPG; ++u) {
-                  const int r = r0 + u;
-                  sa[kb][r] = i == 0 ? pr[u] * dp[kb][r] : pr[u] * (dp[kb][r] + dd);
+                  for (int u = 0; u < DTA_DQ_EXPG; u += 2) {
+                    const int r = r0 + u;
+                    const f32x2 p2 = f32x2{pr[u], pr[u + 1]}, d2 = f32x2{dp[kb][r], dp[kb][r + 1]};
+                    const f32x2 s2 = i == 0 ? p2 * d2 : p2 * (d2 + f32x2{dd, dd});
+                    sa[kb][r] = s2[0];
+                    sa[kb][r + 1] = s2[1];
+                  }
+                } else {
+#pragma unroll
+                  for (int u = 0; u < DTA_DQ_EXPG; ++u) {
+                    const int r = r0 + u;
+                    sa[kb][r] = i == 0 ? pr[u] * dp[kb][r] : pr[u] * (dp[kb][r] + dd);
+                  }
                 }
               }
           } else {
@@ -2380,6 +2421,7 @@ void attn_dkdv_kernel(BwdParams p) {
           });
         }
         // sa[r] = S'_i[q0 + rowof(r)][krow] - LSE; rows 4g..4g+3 of a lane are consecutive
+        constexpr bool PK = DTA_DKDV_PK && !DROP && DK && CFOLD;   // (the unfolded SRD plan spills 18 VGPRs with it)
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           f32x4 d4 = f32x4{};
@@ -2398,9 +2440,31 @@ void attn_dkdv_kernel(BwdParams p) {
               const float mk = drop_mul(dkey[i], q0 + (r & 3) + 8 * (r >> 2) + 4 * hf, krow, p.drop_thr, p.drop_scale);
               if constexpr (DVV) pc[r] = fmaf(coef[i] * mk, pr, pc[r]);
               if constexpr (DK) sa[r] = pr * fmaf(mk, dpa[r], -d4[j]);
+            } else if constexpr (PK) {
+              sa[r] = pr;                 // the pair math below, two rows per packed op
             } else {
               if constexpr (DVV) pc[r] = i == 0 ? (CFOLD ? pr : wv[0] * pr) : fmaf(wv[i], pr, pc[r]);
               if constexpr (DK) sa[r] = i == 0 ? pr * dpa[r] : pr * (dpa[r] + d4[j]);
+            }
+          }
+          if constexpr (PK) {
+            // v_pk_mul_f32 / v_pk_add_f32 / v_pk_fma_f32: two rows per VALU issue (the same
+            // fp32 arithmetic per element, so results are bitwise those of the scalar form)
+#pragma unroll
+            for (int j = 0; j < 4; j += 2) {
+              const int r = 4 * g + j;
+              const f32x2 pr2 = f32x2{sa[r], sa[r + 1]};
+              const f32x2 dp2 = f32x2{dpa[r], dpa[r + 1]};
+              if constexpr (DVV) {
+                f32x2 pc2 = f32x2{pc[r], pc[r + 1]};
+                if (i == 0) pc2 = CFOLD ? pr2 : f32x2{wv[0], wv[0]} * pr2;
+                else pc2 = __builtin_elementwise_fma(f32x2{wv[i], wv[i]}, pr2, pc2);
+                pc[r] = pc2[0]; pc[r + 1] = pc2[1];
+              }
+              f32x2 s2;
+              if (i == 0) s2 = pr2 * dp2;
+              else s2 = pr2 * (dp2 + f32x2{d4[j], d4[j + 1]});
+              sa[r] = s2[0]; sa[r + 1] = s2[1];
             }
           }
         }
