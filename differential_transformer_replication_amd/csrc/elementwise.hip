@@ -284,7 +284,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnParams p) {
 #ifndef DTA_LN_BWD_PD
 #define DTA_LN_BWD_PD 3          // row groups in flight ahead of the one being computed (1..5)
 #endif
-template <class E, int CHB, class Y = E, int RPI = DTA_LN_BWD_RPI, int PD = DTA_LN_BWD_PD>
+// (rows wider than 2048 columns keep one row ahead: they already hold CHB times the bytes in
+// flight per row, and three rows of them cost 206-512 registers, a wave per SIMD or spills)
+template <class E, int CHB, class Y = E, int RPI = DTA_LN_BWD_RPI, int PD = (CHB == 1 ? DTA_LN_BWD_PD : 1)>
 __global__ __launch_bounds__(256) void ln_bwd_rb_kernel(LnParams p) {
   static_assert(PD >= 1 && PD <= 5, "prefetch depth");
   constexpr int NSL = PD + 1;      // register slots of raw rows
