@@ -595,3 +595,40 @@ def test_backward_reductions_are_reproducible():
         grads.append([t.grad.clone() for t in (xg, cg, wg, bg)])
     for a, b_ in zip(*grads):
         assert torch.equal(a, b_)
+
+
+@pytest.mark.parametrize("rows", [1, 9, 513, 5003])
+@pytest.mark.parametrize("dtype,C", [(torch.bfloat16, 2048), (torch.float32, 256), ("mixed", 1024)])
+def test_ln_bwd_row_ring_ragged(rows, dtype, C):
+    """The LayerNorm backward's register ring (three row groups in flight for rows up to 2048
+    columns, round 6) and its one-launch ordered dw/db reduce at row counts that leave the
+    ring part-filled: fewer rows than workgroups, 513 (the 512-workgroup cap plus one), and
+    5003 (~9.8 rows per workgroup).  "mixed": fp32 x normalised into bf16 y, bf16 dy
+    (dta_ln_args.io_dtype, the Blocks' LayerNorm under autocast).  Against fp64 torch
+    (diff_transformer.py:15-20 restated), and dw / db bitwise reproducible run to run."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(rows * 7 + C)
+    x = torch.randn(rows, C, generator=g) * 2 + 0.5
+    w = 1 + 0.1 * torch.randn(C, generator=g)
+    b = 0.1 * torch.randn(C, generator=g)
+    dy = torch.randn(rows, C, generator=g)
+    xdt = torch.float32 if dtype == "mixed" else dtype
+    ydt = torch.bfloat16 if dtype == "mixed" else dtype
+    xq = x.to(xdt).double().requires_grad_(True)
+    w64, b64 = w.double().requires_grad_(True), b.double().requires_grad_(True)
+    ref = orc.group_layer_norm(xq, w64, b64) * 0.2
+    ref.backward(dy.to(ydt).double())
+    grads = []
+    for _ in range(2):
+        xg = x.to(xdt).to(DEV).requires_grad_(True)
+        wg, bg = w.to(DEV).requires_grad_(True), b.to(DEV).requires_grad_(True)
+        out = ops._GroupLNScale.apply(xg, wg, bg, 1e-5, 0.2, None, ydt if dtype == "mixed" else None)
+        assert out.dtype == ydt
+        out.backward(dy.to(ydt).to(DEV))
+        grads.append((wg.grad.clone(), bg.grad.clone()))
+    tol = TOL[torch.bfloat16] if ydt == torch.bfloat16 else TOL[torch.float32]
+    assert rel_err(out.float().cpu(), ref) < tol
+    assert rel_err(xg.grad.float().cpu(), xq.grad) < tol
+    assert rel_err(wg.grad.cpu(), w64.grad) < tol
+    assert rel_err(bg.grad.cpu(), b64.grad) < tol
+    assert torch.equal(grads[0][0], grads[1][0]) and torch.equal(grads[0][1], grads[1][1])
