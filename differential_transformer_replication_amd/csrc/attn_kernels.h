@@ -1617,6 +1617,7 @@ void attn_dq_kernel(BwdParams p) {
   // ---- per-row operands in registers: Q_i and dO rows (B operands), LSE, delta
   frag qf[NQR > 0 ? NQR : 1][NQR > 0 ? NSQ : 1], df[NSV];
   float coef[N], lse[N], del[N];
+  float dhead = 0.f;                 // delta of the current dK/dV group's first branch (delta rows below)
   const int64_t rs = (((int64_t)0 * p.B + b) * p.H + hh) * T + qrow;     // [i][b][h][t], i = 0
   const int64_t bstride = (int64_t)p.B * p.H * T;
 #pragma unroll
@@ -1660,9 +1661,12 @@ void attn_dq_kernel(BwdParams p) {
     d = wave_sum_halves(d);
     del[i] = d;
     // row constants for attn_dkdv, which folds c_i into its dK_i epilogue: without
-    // dropout -delta_0 (its dP accumulator's seed) and delta_0 - delta_i (i >= 1);
-    // with dropout delta_i
-    if (rowok && hf == 0) p.delta[rs + i * bstride] = DROP ? d : (i == 0 ? -d : del[0] - d);
+    // dropout -delta_h (its dP accumulator's seed) at each dK/dV group's first branch h and
+    // delta_h - delta_i after it -- h = 0 (this group), or the dK/dV grouping's starts
+    // (p.kstarts, this launch holding every branch); with dropout delta_i
+    const bool kstart = i == 0 || (DTA_DQ_KSTARTS && ((p.kstarts >> i) & 1));
+    if (kstart) dhead = d;
+    if (rowok && hf == 0) p.delta[rs + i * bstride] = DROP ? d : (kstart ? -d : dhead - d);
     // d(coef)[h][i] = sum over rows of delta_i: one atomic per wave
     float w = (rowok && hf == 0) ? d : 0.f;
 #pragma unroll

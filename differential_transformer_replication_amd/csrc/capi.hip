@@ -335,14 +335,18 @@ int dta_attn_bwd(const dta_attn_bwd_args* a, void* stream) {
   const uint64_t qstarts = rebase ? group_starts(a->dtype, p.HS, p.N, p.DV, qcap) : 0;
   const uint64_t kstarts = rebase ? group_starts(a->dtype, p.HS, p.N, p.DV, kcap) : 0;
   if (stages & DTA_BWD_DQ) {
+    // one dQ launch over every branch writes the delta rows straight in the dK/dV encoding
+    const bool direct = DTA_DQ_KSTARTS && qstarts != kstarts && branch_group(a->dtype, p.HS, p.N, p.DV, qcap) == p.N;
     for (int g0 = 0, ng; g0 < p.N; g0 += ng) {
       ng = branch_group(a->dtype, p.HS, p.N - g0, p.DV, qcap);
-      if ((e = launch_attn_dq(a->dtype, group(g0, ng), st))) return status(e);
+      BwdParams q = group(g0, ng);
+      q.kstarts = direct ? kstarts : 0;
+      if ((e = launch_attn_dq(a->dtype, q, st))) return status(e);
     }
     if (p.dcoef_part &&
         (e = launch_dcoef_reduce(p.dcoef_part, p.dcoef, p.H, p.N, (int64_t)p.B * nblk, st)))
       return status(e);
-    if (qstarts != kstarts && (e = launch_delta_rebase(p.delta, rowvec, p.N, qstarts, kstarts, st)))
+    if (!direct && qstarts != kstarts && (e = launch_delta_rebase(p.delta, rowvec, p.N, qstarts, kstarts, st)))
       return status(e);
   }
   if (stages & DTA_BWD_DKDV) {

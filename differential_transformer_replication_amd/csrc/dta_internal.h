@@ -4,6 +4,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#ifndef DTA_DQ_KSTARTS
+#define DTA_DQ_KSTARTS 1   // attn_dq writes the delta rows in the dK/dV grouping's encoding when it holds every branch (no rebase launch)
+#endif
+
 namespace dta {
 
 struct T5 {            // [b][t][h][i] element strides + base pointer
@@ -58,6 +62,8 @@ struct BwdParams {
   int ob16;            // obr holds fp16 O_i (ABI 6)
   float* lsec;         // optional (ABI 8 lse_c, 16-bit, no dropout): stored LSE_i + log2|c_i| rows
                        // [i][b][h][t], written by attn_dq, the S seeds of attn_dkdv (|c_i| folded into P)
+  uint64_t kstarts;    // attn_dq run as one group, no dropout: the dK/dV grouping's starts (bit i), so the
+                       // delta rows are written in that encoding and no rebase launch follows (0: own group)
 };
 
 // per-dtype launchers (dtype index: 0 bf16, 1 f16, 2 f32); return hipError_t
