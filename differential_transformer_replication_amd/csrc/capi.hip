@@ -98,9 +98,11 @@ int branch_group(int dtype, int hs, int left, int dv, int cap) {
 // 3.4 ms, hs 128 N = 4 8.4 -> 2.9 ms; dQ hs 128 N = 4 4.0 -> 2.0 ms, but dQ at hs 64 / 96
 // N = 3 0.40 -> 0.45 / 1.69 -> 1.84 ms and hs 96 N = 4 2.27 -> 2.35 ms, so dQ groups at
 // head size 128, and at 64 for N >= 4 (0.487 either way: no re-base needed).  Head size 32
-// keeps the native plans for both.  Where the two groupings differ, the dQ stage re-bases
-// the delta rows (delta_rebase_kernel, ~3-7 us) onto the dK/dV grouping
-// (profiles/r04_bwd_rebase.json).  DTA_BWD_GROUP_MAX (A/B builds) overrides both.
+// keeps the native plans for both.  Where the two groupings differ, the delta rows take the
+// dK/dV grouping's encoding: written so by attn_dq when one dQ launch holds every branch
+// (round 6, BwdParams::kstarts, profiles/r06t_ab_dq_kstarts.json), else re-based after the
+// dQ launches (delta_rebase_kernel, ~3-7 us, profiles/r04_bwd_rebase.json).
+// DTA_BWD_GROUP_MAX (A/B builds) overrides both caps.
 int bwd_group_cap(int dtype, int hs, int n, bool dkdv) {
 #ifdef DTA_BWD_GROUP_MAX
   return DTA_BWD_GROUP_MAX;
