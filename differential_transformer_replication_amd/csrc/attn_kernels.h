@@ -629,6 +629,15 @@ inline bool kv_layout_ok(const P& p, int es) {
 //   dP'  = dO V^T - delta_0
 // P_i = exp2(S'_i) with no fma; dS_0 / c_0 = P_0 dP', dS_i / c_i = P_i (dP' + delta_0 -
 // delta_i); c_i and the softmax scale are applied once in the dQ epilogue.
+#ifndef DTA_FWD_IGLP
+#define DTA_FWD_IGLP -1          // A/B: __builtin_amdgcn_iglp_opt(k) in the tile loop (-1 = off); k = 0: no effect on any kernel (r06u), 1: compiler out of memory
+#endif
+#ifndef DTA_DQ_IGLP
+#define DTA_DQ_IGLP -1
+#endif
+#ifndef DTA_DKDV_IGLP
+#define DTA_DKDV_IGLP -1
+#endif
 #ifndef DTA_DQ_SEED
 #define DTA_DQ_SEED 1
 #endif
@@ -1274,6 +1283,7 @@ void attn_fwd_kernel(FwdParams p) {
     st.lap<7>();
     if (kt + NS - 1 < ntiles) stage_kv(kt + NS - 1, (kt + NS - 1) % NS);
     st.lap<0>();
+    if constexpr (DTA_FWD_IGLP >= 0) __builtin_amdgcn_iglp_opt(DTA_FWD_IGLP >= 0 ? DTA_FWD_IGLP : 0);   // A/B: LLVM's MFMA / LDS interleave strategy
     if (live) {
       frag pf[N][NKB * SPB];
       phase_a(kt, MASKED, pf, FASTT);
@@ -1748,6 +1758,7 @@ void attn_dq_kernel(BwdParams p) {
     const int buf = kt % NS;
     if (kt + NS - 1 < ntiles) stage_kv(kt + NS - 1, (kt + NS - 1) % NS);
     st.lap<0>();
+    if constexpr (DTA_DQ_IGLP >= 0) __builtin_amdgcn_iglp_opt(DTA_DQ_IGLP >= 0 ? DTA_DQ_IGLP : 0);   // A/B: LLVM's MFMA / LDS interleave strategy
     const int k0 = kt * BN;
     if (wave_live && k0 <= qw0 + 31) {
       const E* Kc = Kb + buf * CF::nK;
@@ -2323,6 +2334,7 @@ void attn_dkdv_kernel(BwdParams p) {
     const int q0 = kb0 + t * BQ;
     if (t + NS - 1 < ntiles) stage_q(q0 + (NS - 1) * BQ, (t + NS - 1) % NS);
     st.lap<0>();
+    if constexpr (DTA_DKDV_IGLP >= 0) __builtin_amdgcn_iglp_opt(DTA_DKDV_IGLP >= 0 ? DTA_DKDV_IGLP : 0);   // A/B: LLVM's MFMA / LDS interleave strategy
     if (wave_keys && q0 + 31 >= kw0) {
       const char* sg = ringb + buf * RG::SB;
       const E* Qc = SRD ? reinterpret_cast<const E*>(sg) : Qb + buf * N * BQ * HSP;
